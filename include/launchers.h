@@ -1,0 +1,123 @@
+/*
+ * launchers.h -- C-ABI of the MI355X-native quantized multi-head attention library.
+ *
+ * Drop-in for the reference's include/launchers.h (MattJBorowski1991/QuantizedMHA).
+ * Plain C types only: device pointers, sizes and an opaque stream handle (hipStream_t
+ * passed as void*), so cgo/ctypes/JNI/N-API bindings need no HIP or torch headers.
+ *
+ * Libraries (built by tools/build.py):
+ *   libqmha.so                 every entry point below; `solve` bound to fa_tc_int8_b
+ *   libqmha_fa_tc_int8_b.so    `solve` bound to the INT8 path      (make KERNEL=fa_tc_int8_b)
+ *   libqmha_fa_tc_v1a.so       `solve` bound to the FP16 MFMA path (make KERNEL=fa_tc_v1a)
+ *   libqmha_fa.so              `solve` bound to the scalar path    (make KERNEL=fa)
+ *   libqmha_unfused.so         `solve` bound to the 3-kernel path  (make KERNEL=unfused)
+ * mirroring the reference's one-kernel-per-binary build (Makefile:39-53,
+ * extensions/torch/setup.py:21-43).
+ */
+#ifndef QMHA_LAUNCHERS_H
+#define QMHA_LAUNCHERS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Kernel variants (names as in the reference's mha_kernels/ and setup.py:114-124). */
+typedef enum {
+    QMHA_FA = 0,           /* mha_kernels/fa.cu         : fp32 scalar, no matrix cores   */
+    QMHA_FA_TC_V1A = 1,    /* mha_kernels/fa_tc_v1a.cu  : fp16 MFMA, fp32 accumulation   */
+    QMHA_FA_TC_INT8_B = 2, /* mha_kernels/fa_tc_int8_b.cu: int8 MFMA, per-32-row scales  */
+    QMHA_UNFUSED = 3       /* mha_kernels/unfused.cu    : QK^T, softmax, PV (3 kernels)   */
+} qmha_variant_t;
+
+/* Status codes of the extended entry points. */
+enum {
+    QMHA_OK = 0,
+    QMHA_ERR_INVALID = 1, /* shape/argument precondition failed (checked before launch) */
+    QMHA_ERR_HIP = 2,     /* a HIP runtime call or kernel launch failed                  */
+    QMHA_ERR_NOMEM = 3,   /* workspace allocation failed                                 */
+    QMHA_ERR_NOSYS = 4    /* variant / head size not built into this library             */
+};
+
+/*
+ * solve -- replaces the reference's `extern "C" void solve(...)` declared at
+ * include/launchers.h:9-10 and defined per kernel (e.g. mha_kernels/fa_tc_int8_b.cu:600-609).
+ *
+ * Q, K, V, output: DEVICE pointers, fp32, contiguous [N, d_model] row-major; head k owns
+ * columns [k*d, (k+1)*d), d = d_model / h.  output is fully overwritten.
+ * Blocking: the result is complete on return (reference launchers.h:64).  Scratch is
+ * owned by the library.  Preconditions (the reference asserts N % 32 on the device,
+ * fa_tc_int8_b.cu:422-423): N % 32 == 0, d_model == h*d, d in {32, 64, 128}.  The
+ * reference's d is a compile-time constant (config.h:28); here it is a runtime value.
+ * On a violated precondition or HIP error `solve` prints one line to stderr and returns
+ * (the reference returns void and ignores errors).
+ */
+void solve(const float *Q, const float *K, const float *V, float *output, int N, int d_model, int h);
+
+/*
+ * qmha_solve_ex -- batched, asynchronous, status-returning form of `solve`.
+ * Q/K/V/O are [B, N, d_model] fp32 device tensors (batch outermost; B calls of the
+ * reference `solve`).  Work is enqueued on `stream` (hipStream_t, NULL = default stream)
+ * and the call returns without synchronising.  A library-owned workspace is cached per
+ * (device, stream); see qmha_solve_ws for caller-owned scratch (graph capture).
+ */
+int qmha_solve_ex(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model, int h,
+                  int variant, void *stream);
+
+/* Bytes of scratch qmha_solve_ws needs for this problem (0 for variants without). */
+size_t qmha_workspace_size(int B, int N, int d_model, int h, int variant);
+
+/* As qmha_solve_ex with caller-owned device scratch of >= qmha_workspace_size bytes
+ * (256-byte aligned).  Makes no allocation and no synchronisation: capturable in a hipGraph. */
+int qmha_solve_ws(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model, int h,
+                  int variant, void *workspace, size_t workspace_bytes, void *stream);
+
+/* Blocking convenience used by the per-variant `solve` shims and the JAX raw-pointer
+ * binding (extensions/jax/jax_ext.cpp:12-28): batch 1, synchronises the device stream. */
+int qmha_solve_variant(const float *Q, const float *K, const float *V, float *O, int N, int d_model, int h,
+                       int variant);
+
+/*
+ * qmha_quantize_int8 -- the INT8 path's pre-pass as a standalone op:
+ * per 32-row group of every head, scale = max(absmax/127, 1e-8) and
+ * x_i8 = clamp(rint(x / scale), -128, 127) (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
+ * X: [B, N, d_model] fp32 device.  Xi: [B][h][N][d] int8 device.  scales: [B][h][N/32].
+ * layout 0 = row-major rows (Q, K operand); layout 1 = V^T MFMA operand order
+ * ([B][h][N/32][d][32], kv slots permuted as documented in DESIGN.md).
+ */
+int qmha_quantize_int8(const float *X, int B, int N, int d_model, int h, int8_t *Xi, float *scales, int layout,
+                       void *stream);
+
+/*
+ * qmha_debug_qk_int32 -- test hook for the bit-exact KAT: quantises Q and K exactly as the
+ * INT8 path does and writes S = Q_i8 K_i8^T (int32) of head `head` (batch 0) computed by
+ * the same v_mfma_i32_32x32x32_i8 operand path into S[N][N] (device).  Blocking.
+ */
+int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int h, int head, int32_t *S);
+
+/* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused") -> id, or -1. */
+int qmha_variant_from_name(const char *name);
+const char *qmha_variant_name(int variant);
+const char *qmha_status_string(int status);
+const char *qmha_version(void);
+/* Last HIP error string recorded by a failing call on this thread ("" if none). */
+const char *qmha_last_error(void);
+
+/*
+ * Kernel timing for roofline reporting (bench.py): when enabled, qmha_solve_* record a
+ * hipEvent pair around the dominant ("main") kernel of every call.  qmha_profile_collect
+ * synchronises those events and returns the summed main-kernel milliseconds and the
+ * launch count since the last collect, then clears the record.
+ */
+void qmha_profile_enable(int on);
+int qmha_profile_collect(double *main_ms, long long *launches, double *prepass_ms);
+
+/* Release all library-owned workspaces (optional; also released at process exit). */
+void qmha_release_workspaces(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QMHA_LAUNCHERS_H */

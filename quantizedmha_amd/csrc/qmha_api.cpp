@@ -1,0 +1,373 @@
+// qmha_api.cpp -- the C-ABI (include/launchers.h): argument checks, workspace ownership,
+// variant dispatch, profiling hooks.  Replaces the reference's launch<KernelFn> per-head
+// slicer (include/launchers.h:16-72): no per-call cudaMalloc/cudaFree, no extract/concat
+// copies (kernels read and write the strided [N, d_model] head slices directly), all B*H
+// heads in one grid, and errors are reported instead of ignored.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/launchers.h"
+#include "qmha_kernels.hpp"
+
+#define QMHA_VERSION_STRING "qmha-mi355x 0.1.0 (gfx950)"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return QMHA_ERR_HIP;
+}
+
+#define QMHA_HIP_TRY(expr, what)                 \
+    do {                                         \
+        hipError_t _e = (expr);                  \
+        if (_e != hipSuccess) return hip_fail(_e, what); \
+    } while (0)
+
+int check_shape(const void* Q, const void* K, const void* V, const void* O, int B, int N, int d_model, int h,
+                int variant, int* D_out) {
+    if (!Q || !K || !V || !O) {
+        g_last_error = "null tensor pointer";
+        return QMHA_ERR_INVALID;
+    }
+    if (B < 1 || N < 1 || d_model < 1 || h < 1) {
+        g_last_error = "B, N, d_model and h must be positive";
+        return QMHA_ERR_INVALID;
+    }
+    if (d_model % h != 0) {  // config.h:27
+        g_last_error = "d_model must be divisible by h";
+        return QMHA_ERR_INVALID;
+    }
+    if (N % 32 != 0) {  // fa_tc_int8_b.cu:422-423 (N % Br), Br = Bc = 32
+        g_last_error = "N must be a multiple of 32";
+        return QMHA_ERR_INVALID;
+    }
+    const int D = d_model / h;
+    if (D != 32 && D != 64 && D != 128) {  // config.h:32 requires d % 32 == 0
+        g_last_error = "head size d = d_model/h must be 32, 64 or 128";
+        return QMHA_ERR_NOSYS;
+    }
+    if (variant < QMHA_FA || variant > QMHA_UNFUSED) {
+        g_last_error = "unknown variant";
+        return QMHA_ERR_INVALID;
+    }
+    if ((size_t)B * N * d_model > (size_t)INT32_MAX * 4) {
+        g_last_error = "tensor too large";
+        return QMHA_ERR_INVALID;
+    }
+    *D_out = D;
+    return QMHA_OK;
+}
+
+// ---- profiling --------------------------------------------------------------------------
+struct ProfRec {
+    hipEvent_t e0, e1, e2;  // e0 -> e1 pre-pass, e1 -> e2 main kernel
+    bool has_pre;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof_recs;
+std::vector<hipEvent_t> g_event_pool;
+
+hipEvent_t take_event() {
+    if (!g_event_pool.empty()) {
+        hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// ---- library-owned workspaces, one per (device, stream) --------------------------------
+struct WsKey {
+    int dev;
+    void* stream;
+    bool operator<(const WsKey& o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
+};
+struct WsBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_ws_mu;
+std::map<WsKey, WsBuf> g_ws;
+
+int get_workspace(size_t need, hipStream_t stream, void** out) {
+    *out = nullptr;
+    if (need == 0) return QMHA_OK;
+    int dev = 0;
+    QMHA_HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    WsBuf& b = g_ws[WsKey{dev, (void*)stream}];
+    if (b.bytes < need) {
+        if (b.ptr) {
+            // the old buffer may still be read by work queued on this stream
+            QMHA_HIP_TRY(hipStreamSynchronize(stream), "hipStreamSynchronize");
+            (void)hipFree(b.ptr);
+            b.ptr = nullptr;
+            b.bytes = 0;
+        }
+        size_t alloc = qmha::align_up(need + need / 8, 1 << 20);
+        if (hipMalloc(&b.ptr, alloc) != hipSuccess) {
+            b.ptr = nullptr;
+            g_last_error = "hipMalloc of workspace failed";
+            return QMHA_ERR_NOMEM;
+        }
+        b.bytes = alloc;
+    }
+    *out = b.ptr;
+    return QMHA_OK;
+}
+
+size_t workspace_bytes(int B, int N, int H, int D, int variant) {
+    switch (variant) {
+        case QMHA_FA_TC_INT8_B: return qmha::int8_workspace_bytes(B, N, H, D);
+        case QMHA_FA_TC_V1A: return qmha::f16_workspace_bytes(B, N, H, D);
+        case QMHA_UNFUSED: return qmha::unfused_workspace_bytes(B, N, H, D);
+        default: return 0;
+    }
+}
+
+int run(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model, int h, int variant,
+        void* ws, size_t ws_bytes, hipStream_t stream) {
+    const int D = d_model / h;
+    const size_t need = workspace_bytes(B, N, h, D, variant);
+    if (ws_bytes < need) {
+        g_last_error = "workspace too small";
+        return QMHA_ERR_INVALID;
+    }
+    ProfRec rec{nullptr, nullptr, nullptr, false};
+    bool prof;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        prof = g_prof_on;
+        if (prof) {
+            rec.e0 = take_event();
+            rec.e1 = take_event();
+            rec.e2 = take_event();
+            if (!rec.e0 || !rec.e1 || !rec.e2) prof = false;
+        }
+    }
+    if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e0, stream), "hipEventRecord");
+    switch (variant) {
+        case QMHA_FA_TC_INT8_B: {
+            qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
+            QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, B, N, h, D, d_model, stream), "quant_int8 launch");
+            rec.has_pre = true;
+            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
+            QMHA_HIP_TRY(qmha::launch_fa_int8_main(w, O, B, N, h, D, d_model, stream), "fa_int8 launch");
+            break;
+        }
+        case QMHA_FA_TC_V1A: {
+            qmha::F16Workspace w = qmha::f16_carve(ws, B, N, h, D);
+            QMHA_HIP_TRY(qmha::launch_convert_f16(Q, K, V, w, B, N, h, D, d_model, stream), "convert_f16 launch");
+            rec.has_pre = true;
+            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
+            QMHA_HIP_TRY(qmha::launch_fa_f16_main(w, O, B, N, h, D, d_model, stream), "fa_f16 launch");
+            break;
+        }
+        case QMHA_FA: {
+            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
+            QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, stream), "fa_f32 launch");
+            break;
+        }
+        case QMHA_UNFUSED: {
+            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
+            QMHA_HIP_TRY(qmha::launch_unfused(Q, K, V, O, ws, B, N, h, D, d_model, stream), "unfused launch");
+            break;
+        }
+        default:
+            g_last_error = "unknown variant";
+            return QMHA_ERR_INVALID;
+    }
+    if (prof) {
+        QMHA_HIP_TRY(hipEventRecord(rec.e2, stream), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof_recs.push_back(rec);
+    }
+    return QMHA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qmha_solve_ws(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model, int h,
+                  int variant, void* workspace, size_t workspace_bytes_, void* stream) {
+    int D = 0;
+    int st = check_shape(Q, K, V, O, B, N, d_model, h, variant, &D);
+    if (st != QMHA_OK) return st;
+    return run(Q, K, V, O, B, N, d_model, h, variant, workspace, workspace_bytes_, (hipStream_t)stream);
+}
+
+int qmha_solve_ex(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model, int h,
+                  int variant, void* stream) {
+    int D = 0;
+    int st = check_shape(Q, K, V, O, B, N, d_model, h, variant, &D);
+    if (st != QMHA_OK) return st;
+    const size_t need = workspace_bytes(B, N, h, D, variant);
+    void* ws = nullptr;
+    st = get_workspace(need, (hipStream_t)stream, &ws);
+    if (st != QMHA_OK) return st;
+    return run(Q, K, V, O, B, N, d_model, h, variant, ws, need, (hipStream_t)stream);
+}
+
+size_t qmha_workspace_size(int B, int N, int d_model, int h, int variant) {
+    if (B < 1 || N < 1 || h < 1 || d_model % h) return 0;
+    return workspace_bytes(B, N, h, d_model / h, variant);
+}
+
+int qmha_solve_variant(const float* Q, const float* K, const float* V, float* O, int N, int d_model, int h,
+                       int variant) {
+    int st = qmha_solve_ex(Q, K, V, O, 1, N, d_model, h, variant, nullptr);
+    if (st != QMHA_OK) return st;
+    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    return QMHA_OK;
+}
+
+int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t* Xi, float* scales, int layout,
+                       void* stream) {
+    int D = 0;
+    int st = check_shape(X, X, X, Xi, B, N, d_model, h, QMHA_FA_TC_INT8_B, &D);
+    if (st != QMHA_OK) return st;
+    if (!scales || (layout != 0 && layout != 1)) {
+        g_last_error = "bad scales pointer or layout";
+        return QMHA_ERR_INVALID;
+    }
+    // The pre-pass quantises Q, K, V in one launch; run it with X in the requested role and
+    // write only that role's output (the other two roles go to a scratch workspace).
+    const size_t need = qmha::int8_workspace_bytes(B, N, h, D);
+    void* ws = nullptr;
+    st = get_workspace(need, (hipStream_t)stream, &ws);
+    if (st != QMHA_OK) return st;
+    qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
+    if (layout == 0) {
+        w.Qi = Xi;
+        w.sQ = scales;
+    } else {
+        w.Vt = Xi;
+        w.sV = scales;
+    }
+    QMHA_HIP_TRY(qmha::launch_quant_int8(X, X, X, w, B, N, h, D, d_model, (hipStream_t)stream), "quant_int8 launch");
+    return QMHA_OK;
+}
+
+int qmha_debug_qk_int32(const float* Q, const float* K, int N, int d_model, int h, int head, int32_t* S) {
+    int D = 0;
+    int st = check_shape(Q, K, Q, S, 1, N, d_model, h, QMHA_FA_TC_INT8_B, &D);
+    if (st != QMHA_OK) return st;
+    if (head < 0 || head >= h) {
+        g_last_error = "head out of range";
+        return QMHA_ERR_INVALID;
+    }
+    const size_t need = qmha::int8_workspace_bytes(1, N, h, D);
+    void* ws = nullptr;
+    st = get_workspace(need, nullptr, &ws);
+    if (st != QMHA_OK) return st;
+    qmha::Int8Workspace w = qmha::int8_carve(ws, 1, N, h, D);
+    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, Q, w, 1, N, h, D, d_model, nullptr), "quant_int8 launch");
+    QMHA_HIP_TRY(qmha::launch_debug_qk_int32(w, N, D, head, S, nullptr), "debug_qk launch");
+    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    return QMHA_OK;
+}
+
+int qmha_variant_from_name(const char* name) {
+    if (!name) return -1;
+    if (!std::strcmp(name, "fa")) return QMHA_FA;
+    if (!std::strcmp(name, "fa_tc_v1a")) return QMHA_FA_TC_V1A;
+    if (!std::strcmp(name, "fa_tc_int8_b")) return QMHA_FA_TC_INT8_B;
+    if (!std::strcmp(name, "unfused")) return QMHA_UNFUSED;
+    return -1;
+}
+
+const char* qmha_variant_name(int v) {
+    switch (v) {
+        case QMHA_FA: return "fa";
+        case QMHA_FA_TC_V1A: return "fa_tc_v1a";
+        case QMHA_FA_TC_INT8_B: return "fa_tc_int8_b";
+        case QMHA_UNFUSED: return "unfused";
+        default: return "unknown";
+    }
+}
+
+const char* qmha_status_string(int s) {
+    switch (s) {
+        case QMHA_OK: return "ok";
+        case QMHA_ERR_INVALID: return "invalid argument";
+        case QMHA_ERR_HIP: return "HIP error";
+        case QMHA_ERR_NOMEM: return "out of device memory";
+        case QMHA_ERR_NOSYS: return "not supported";
+        default: return "unknown status";
+    }
+}
+
+const char* qmha_version(void) { return QMHA_VERSION_STRING; }
+
+const char* qmha_last_error(void) { return g_last_error.c_str(); }
+
+void qmha_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+}
+
+int qmha_profile_collect(double* main_ms, long long* launches, double* prepass_ms) {
+    std::vector<ProfRec> recs;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        recs.swap(g_prof_recs);
+    }
+    double tm = 0.0, tp = 0.0;
+    for (auto& r : recs) {
+        QMHA_HIP_TRY(hipEventSynchronize(r.e2), "hipEventSynchronize");
+        float a = 0.0f, b = 0.0f;
+        QMHA_HIP_TRY(hipEventElapsedTime(&a, r.e1, r.e2), "hipEventElapsedTime");
+        tm += a;
+        if (r.has_pre) {
+            QMHA_HIP_TRY(hipEventElapsedTime(&b, r.e0, r.e1), "hipEventElapsedTime");
+            tp += b;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        for (auto& r : recs) {
+            g_event_pool.push_back(r.e0);
+            g_event_pool.push_back(r.e1);
+            g_event_pool.push_back(r.e2);
+        }
+    }
+    if (main_ms) *main_ms = tm;
+    if (prepass_ms) *prepass_ms = tp;
+    if (launches) *launches = (long long)recs.size();
+    return QMHA_OK;
+}
+
+void qmha_release_workspaces(void) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& kv : g_ws) {
+        if (kv.second.ptr) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(kv.second.ptr);
+        }
+    }
+    g_ws.clear();
+}
+
+#ifndef QMHA_NO_DEFAULT_SOLVE
+// libqmha.so's `solve` = the north-star drop-in target, fa_tc_int8_b.
+void solve(const float* Q, const float* K, const float* V, float* output, int N, int d_model, int h) {
+    int st = qmha_solve_variant(Q, K, V, output, N, d_model, h, QMHA_FA_TC_INT8_B);
+    if (st != QMHA_OK) std::fprintf(stderr, "qmha solve(fa_tc_int8_b): %s: %s\n", qmha_status_string(st), qmha_last_error());
+}
+#endif
+
+}  // extern "C"

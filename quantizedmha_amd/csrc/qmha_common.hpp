@@ -1,0 +1,114 @@
+// qmha_common.hpp -- shared device/host helpers for the MI355X (gfx950) attention path.
+//
+// Layout vocabulary used throughout (DESIGN.md "Data layout in HBM"):
+//   X      : caller fp32 tensor [B][N][d_model], head k owns columns [k*D, (k+1)*D)
+//            (reference include/launchers.h:42,50-52).
+//   group  : 32 consecutive sequence rows of one head -- the reference's Br = Bc = 32
+//            quantisation block (include/config.h:10-11, fa_tc_int8_b.cu:484,496,518).
+//   bh     : flattened (batch, head) index, b*H + k.
+//   Xi     : int8 [bh][N][D] row-major (Q, K after the pre-pass).
+//   Vt     : V as the MFMA "V^T" operand: per group a [D][32] block whose 32 kv slots are
+//            permuted so that byte 16*h + e of row d holds kv = (e&3) + 8*(e>>2) + 4*h,
+//            i.e. exactly the kv order in which a 32x32 MFMA accumulator hands P^T to a
+//            lane (see kv_of_slot_i8 below).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define QMHA_GROUP 32
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+typedef _Float16 v2h __attribute__((ext_vector_type(2)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// --------------------------------------------------------------------------
+// MFMA accumulator maps (gfx950, every 32x32 shape):
+//   lane l, register r  ->  column = l & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)
+// With the "swapped" products used by every kernel here (S^T = K Q^T and O^T = V^T P^T)
+// the column is the query row, so all per-query statistics are lane-local.
+// --------------------------------------------------------------------------
+__host__ __device__ constexpr int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// int8 32x32x32: operand element e (0..15) of lane half h pairs with accumulator row
+// acc_row(e, h) of the S^T tile, so the V^T operand slot 16*h + e must hold that kv.
+__host__ __device__ constexpr int kv_of_slot_i8(int slot) { return acc_row(slot & 15, slot >> 4); }
+__host__ __device__ constexpr int slot_of_kv_i8(int kv) { return 16 * ((kv >> 2) & 1) + 4 * (kv >> 3) + (kv & 3); }
+
+// f16 32x32x16: k-step s (0,1) takes accumulator registers 8s..8s+7; element e of lane
+// half h pairs with acc_row(8s + e, h) = 16s + 4h + (e & 3) + 8 * (e >> 2).
+__host__ __device__ constexpr int kv_of_slot_f16(int slot) {
+    return 16 * (slot >> 4) + 4 * ((slot >> 3) & 1) + (slot & 3) + 8 * ((slot >> 2) & 1);
+}
+__host__ __device__ constexpr int slot_of_kv_f16(int kv) {
+    return 16 * (kv >> 4) + 8 * ((kv >> 2) & 1) + (kv & 3) + 4 * ((kv >> 3) & 1);
+}
+
+// --------------------------------------------------------------------------
+// cross-lane helpers (wave64)
+// --------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+
+// Combine the two 32-lane halves (lanes l and l^32 hold the same query row).
+__device__ __forceinline__ float half_swap_max(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+    return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ float half_swap_add(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+    return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+__device__ __forceinline__ int half_swap_max_i(int x) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return max((int)r[0], (int)r[1]);
+}
+
+// Max over the 32 lanes of each half (result in every lane of that half).
+__device__ __forceinline__ float half_max32(float x) {
+    x = fmaxf(x, dpp_mov<0xB1>(x));   // quad_perm(1,0,3,2)
+    x = fmaxf(x, dpp_mov<0x4E>(x));   // quad_perm(2,3,0,1)
+    x = fmaxf(x, dpp_mov<0x141>(x));  // row_half_mirror
+    x = fmaxf(x, dpp_mov<0x140>(x));  // row_mirror
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false);
+    return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+
+// Max over all 64 lanes.
+__device__ __forceinline__ float wave_max64(float x) { return half_swap_max(half_max32(x)); }
+
+// --------------------------------------------------------------------------
+// The reference quantiser (fa_tc_int8_b.cu:104-106,136-140), elementwise part.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ float qmha_scale_from_absmax(float absmax) {
+    return fmaxf(absmax / 127.0f, 1e-8f);
+}
+__device__ __forceinline__ int qmha_quant_i8(float v, float inv) {
+    int q = __float2int_rn(v * inv);
+    return q < -128 ? -128 : (q > 127 ? 127 : q);
+}
+
+// Round-half-even of a non-negative x < 2^22 into the low mantissa bits:
+// fma(p, inv, 1.5 * 2^23) is exactly rint(p*inv) + 1.5*2^23.
+#define QMHA_MAGIC_RNE 12582912.0f
+
+__device__ __forceinline__ uint32_t pack4_lowbytes(float a, float b, float c, float d) {
+    uint32_t t01 = __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x0c0c0400u);
+    uint32_t t23 = __builtin_amdgcn_perm(__float_as_uint(d), __float_as_uint(c), 0x0c0c0400u);
+    return __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+}
+
+// XCD-aware remap of a linear workgroup id: the dispatcher deals ids round-robin over the
+// 8 XCDs, so give each XCD a contiguous range of work items (consecutive q-blocks of the
+// same head share K/V in that XCD's L2).  Bijective for any nwg (cdna guide T1).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg / 8, r = nwg % 8;
+    const int xcd = orig % 8, slot = orig / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}

@@ -1,0 +1,290 @@
+// qmha_fa_f16.hip -- fused FP16-MFMA FlashAttention-2 forward for gfx950 (MI355X).
+//
+// Drop-in for the reference's fa_tc_v1a (mha_kernels/fa_tc_v1a.cu:222-439):
+//   Q, K, V -> __float2half (RNE);  S = Qh Kh^T with fp32 accumulation;  s = S / sqrt(d)
+//   online softmax with m0 = 0 (:290): p = exp(s - m), l = alpha*l + sum(p) (fp32 p)
+//   P stored as half(p) (:174);  O = alpha*O + Ph Vh (fp32 accumulate, :218)
+//   out = O / l, 0 if l <= 1e-10 (:384-388)
+//
+// Same skeleton as the INT8 kernel: a conversion pre-pass writes Q/K as f16 rows and V in
+// the f16 V^T operand order; the main kernel keeps Q in registers, streams K/V tiles
+// through double-buffered swizzled LDS and runs both products on v_mfma_f32_32x32x16_f16
+// with swapped operands.  The O accumulator is the MFMA C operand, so the P@V
+// accumulation costs no VALU; alpha == 1 rescales are skipped exactly.
+#include "qmha_common.hpp"
+#include "qmha_kernels.hpp"
+
+namespace qmha {
+
+static constexpr float kLog2eH = 1.4426950408889634f;
+
+template <int D>
+__global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+    _Float16* __restrict__ Qh, _Float16* __restrict__ Kh, _Float16* __restrict__ Vt,
+    int N, int H, int d_model, int total_groups) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
+    __shared__ __attribute__((aligned(16))) _Float16 vtile[4][32 * D];
+    const int tensor = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + wave;
+    const bool active = item < total_groups;
+    const int G = N / QMHA_GROUP;
+    const int bh = active ? item / G : 0, g = active ? item % G : 0;
+    const int b = bh / H, k = bh % H;
+    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
+    const int ri = lane / C4, ci = lane % C4;
+    v4f v[NI];
+    if (active) {
+        const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) v[i] = *reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model);
+    }
+    if (tensor < 2) {
+        if (active) {
+            _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                typedef _Float16 v4h __attribute__((ext_vector_type(4)));
+                v4h hv;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)
+                *reinterpret_cast<v4h*>(dst + (size_t)(i * RPI + ri) * D) = hv;
+            }
+        }
+    } else {
+        _Float16* tile = vtile[wave];
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int slot = slot_of_kv_f16(i * RPI + ri);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (_Float16)v[i][c];
+            }
+        }
+        __syncthreads();
+        if (active) {
+            _Float16* dst = Vt + ((size_t)bh * G + g) * (size_t)(32 * D);
+            constexpr int CH = 32 * D * 2 / 16;
+#pragma unroll
+            for (int c = lane; c < CH; c += 64)
+                reinterpret_cast<v4i*>(dst)[c] = reinterpret_cast<const v4i*>(tile)[c];
+        }
+    }
+}
+
+template <int RB>
+__device__ __forceinline__ int chunk_swz_h(int row) {
+    constexpr int rpb = 256 / RB >= 1 ? 256 / RB : 1;
+    return (row / rpb) & (RB / 16 - 1);
+}
+
+template <int D, int WAVES, int SG>
+__global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
+    const _Float16* __restrict__ Qh, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    constexpr int KS = D / 16;   // QK k-steps (K = 16)
+    constexpr int MB = D / 32;   // PV d-blocks
+    constexpr int RB = 2 * D;    // K row bytes
+    constexpr int STAGE_BYTES = SG * 32 * D * 2;
+    constexpr int NT = WAVES * 64;
+    constexpr int CH = STAGE_BYTES / 16;
+    constexpr int CPT = (CH + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) char lds[2][2 * STAGE_BYTES];
+
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int qg = qb * WAVES + wave;
+    const bool active = qg < G;
+    const int half = lane >> 5, col = lane & 31;
+
+    v8h qop[KS];
+    if (active) {
+        const _Float16* qp = Qh + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 8 * half;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) qop[s] = *reinterpret_cast<const v8h*>(qp + 16 * s);
+    } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qop[s][e] = (_Float16)0.0f;
+    }
+    v16f o[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[m][r] = 0.0f;
+    float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290)
+
+    const char* kbase = reinterpret_cast<const char*>(Kh + (size_t)bh * N * D);
+    const char* vbase = reinterpret_cast<const char*>(Vt + (size_t)bh * N * D);
+    const int nst = (G + SG - 1) / SG;
+    v4i kst[CPT], vst[CPT];
+    auto gload = [&](int st) {
+        const int g0 = st * SG;
+        const int nch = min(SG, G - g0) * 32 * D * 2 / 16;
+        const v4i* ks = reinterpret_cast<const v4i*>(kbase + (size_t)g0 * 32 * D * 2);
+        const v4i* vs = reinterpret_cast<const v4i*>(vbase + (size_t)g0 * 32 * D * 2);
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int idx = tid + c * NT;
+            if (idx < nch) {
+                kst[c] = ks[idx];
+                vst[c] = vs[idx];
+            }
+        }
+    };
+    auto lstore = [&](int buf, int st) {
+        const int g0 = st * SG;
+        const int nch = min(SG, G - g0) * 32 * D * 2 / 16;
+        char* L = lds[buf];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int idx = tid + c * NT;
+            if (idx < nch) {
+                const int row = idx / (RB / 16), cc = idx % (RB / 16);
+                *reinterpret_cast<v4i*>(L + row * RB + 16 * (cc ^ chunk_swz_h<RB>(row))) = kst[c];
+                const int grp = idx / (4 * D), w = idx % (4 * D);  // V rows are 64 B = 4 chunks
+                const int d = w >> 2, cv = w & 3;
+                *reinterpret_cast<v4i*>(L + STAGE_BYTES + grp * 64 * D + d * 64 + 16 * (cv ^ chunk_swz_h<64>(d))) = vst[c];
+            }
+        }
+    };
+
+    gload(0);
+    lstore(0, 0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) gload(st + 1);
+        if (active) {
+            const int g0 = st * SG;
+            const int ngr = min(SG, G - g0);
+            const char* L = lds[buf];
+#pragma unroll
+            for (int gi = 0; gi < SG; ++gi) {
+                if (gi < ngr) {
+                    v16f s = {};
+                    const int krow = gi * 32 + col;
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) {
+                        const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
+                        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
+                    }
+                    float mx = s[0];
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
+                    mx = half_swap_max(mx);
+                    const float m_new = fmaxf(m_run, mx * c_log2);
+                    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                    float rs = 0.0f;
+                    v8h pop[2];
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {
+                        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_new));
+                        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c_log2, -m_new));
+                        rs += p0;
+                        rs += p1;
+                        const v2h h2 = __builtin_convertvector((v2f{p0, p1}), v2h);  // v_cvt_pk_f16_f32 (RNE)
+                        pop[r >> 3][r & 7] = h2[0];
+                        pop[r >> 3][(r & 7) + 1] = h2[1];
+                    }
+                    rs = half_swap_add(rs);
+                    l_run = fmaf(alpha, l_run, rs);  // fa_tc_v1a.cu:198
+                    m_run = m_new;
+                    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
+#pragma unroll
+                        for (int m = 0; m < MB; ++m)
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) o[m][r] *= alpha;
+                    }
+#pragma unroll
+                    for (int m = 0; m < MB; ++m) {
+                        const int d = 32 * m + col;
+                        const char* vr = L + STAGE_BYTES + gi * 64 * D + d * 64;
+#pragma unroll
+                        for (int ks = 0; ks < 2; ++ks) {
+                            const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+        if (st + 1 < nst) lstore(buf ^ 1, st + 1);
+        __syncthreads();
+    }
+    if (active) {
+        const bool ok = l_run > 1e-10f;
+        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                v4f w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = ok ? o[m][4 * g4 + j] / l_run : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
+            }
+    }
+}
+
+size_t f16_workspace_bytes(int B, int N, int H, int D) {
+    return 3 * align_up((size_t)B * H * N * D * 2, 256);
+}
+
+F16Workspace f16_carve(void* ws, int B, int N, int H, int D) {
+    const size_t e = align_up((size_t)B * H * N * D * 2, 256);
+    char* p = static_cast<char*>(ws);
+    F16Workspace w;
+    w.Qh = reinterpret_cast<_Float16*>(p);
+    w.Kh = reinterpret_cast<_Float16*>(p + e);
+    w.Vt = reinterpret_cast<_Float16*>(p + 2 * e);
+    return w;
+}
+
+template <int D>
+static hipError_t convert_f16_d(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
+                                int H, int d_model, hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    hipLaunchKernelGGL((qmha_convert_f16_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.Qh,
+                       w.Kh, w.Vt, N, H, d_model, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
+                              int H, int D, int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return convert_f16_d<32>(Q, K, V, w, B, N, H, d_model, stream);
+        case 64: return convert_f16_d<64>(Q, K, V, w, B, N, H, d_model, stream);
+        case 128: return convert_f16_d<128>(Q, K, V, w, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int D>
+static hipError_t fa_f16_d(const F16Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
+    constexpr int WAVES = 4, SG = 2;
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;  // fa_tc_v1a.cu:421
+    hipLaunchKernelGGL((qmha_fa_f16_kernel<D, WAVES, SG>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qh, w.Kh,
+                       w.Vt, O, N, H, d_model, nqb, c_log2);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,
+                              hipStream_t stream) {
+    switch (D) {
+        case 32: return fa_f16_d<32>(w, O, B, N, H, d_model, stream);
+        case 64: return fa_f16_d<64>(w, O, B, N, H, d_model, stream);
+        case 128: return fa_f16_d<128>(w, O, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace qmha

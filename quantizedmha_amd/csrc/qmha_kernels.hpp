@@ -1,0 +1,52 @@
+// qmha_kernels.hpp -- internal (non-ABI) launcher declarations shared by the kernel
+// translation units and the C-ABI layer (qmha_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace qmha {
+
+inline constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- INT8 (fa_tc_int8_b) ---------------------------------------------------------------
+struct Int8Workspace {
+    int8_t* Qi;  // [B*H][N][D]
+    int8_t* Ki;  // [B*H][N][D]
+    int8_t* Vt;  // [B*H][N/32][D][32]  (i8 operand slot order, qmha_common.hpp)
+    float* sQ;   // [B*H][N/32]
+    float* sK;
+    float* sV;
+};
+size_t int8_workspace_bytes(int B, int N, int H, int D);
+Int8Workspace int8_carve(void* ws, int B, int N, int H, int D);
+hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                             int H, int D, int d_model, hipStream_t stream);
+hipError_t launch_fa_int8_main(const Int8Workspace& w, float* O, int B, int N, int H, int D, int d_model,
+                               hipStream_t stream);
+hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream);
+
+// ---- FP16 (fa_tc_v1a) ------------------------------------------------------------------
+struct F16Workspace {
+    _Float16* Qh;  // [B*H][N][D]
+    _Float16* Kh;  // [B*H][N][D]
+    _Float16* Vt;  // [B*H][N/32][D][32]  (f16 operand slot order)
+};
+size_t f16_workspace_bytes(int B, int N, int H, int D);
+F16Workspace f16_carve(void* ws, int B, int N, int H, int D);
+hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
+                              int H, int D, int d_model, hipStream_t stream);
+hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,
+                              hipStream_t stream);
+
+// ---- FP32 scalar (fa) ------------------------------------------------------------------
+hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int D,
+                         int d_model, hipStream_t stream);
+
+// ---- unfused 3-kernel baseline (unfused.cu) --------------------------------------------
+size_t unfused_workspace_bytes(int B, int N, int H, int D);
+hipError_t launch_unfused(const float* Q, const float* K, const float* V, float* O, void* ws, int B, int N, int H,
+                          int D, int d_model, hipStream_t stream);
+
+}  // namespace qmha

@@ -1,0 +1,137 @@
+"""CPU tests of the drop-in boundary: the C-ABI libraries load and export every symbol
+include/launchers.h declares, host-side argument checks reject bad shapes before any GPU
+call, and the Python mirrors of the reference bindings keep its error behaviour.
+No kernel is launched here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "launchers.h")
+LIB_DIR = os.path.join(ROOT, "quantizedmha_amd", "lib")
+VARIANTS = ["fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused"]
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*([a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+@pytest.fixture(scope="module")
+def built():
+    from tools.build import build
+    build(verbose=False)
+    return True
+
+
+def test_header_declares_reference_solve_signature():
+    src = open(HEADER).read()
+    assert re.search(r"void solve\(const float \*Q, const float \*K, const float \*V, float \*output, int N, "
+                     r"int d_model, int h\);", src)
+
+
+def test_libqmha_exports_every_declared_symbol(built):
+    lib = ctypes.CDLL(os.path.join(LIB_DIR, "libqmha.so"))
+    names = declared_functions()
+    assert "solve" in names and "qmha_solve_ex" in names and len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_variant_libraries_export_solve(built, variant):
+    path = os.path.join(LIB_DIR, f"libqmha_{variant}.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    assert re.search(r" T solve$", out, flags=re.M), out
+    ctypes.CDLL(path)  # resolves libqmha.so through $ORIGIN
+
+
+def test_python_binding_signatures_cover_header(built):
+    from quantizedmha_amd import _lib
+    assert set(declared_functions()) == set(_lib.SIGNATURES)
+    lib = _lib.load()
+    assert lib.qmha_version().decode().startswith("qmha-mi355x")
+
+
+def test_host_side_queries(built):
+    from quantizedmha_amd import _lib
+    lib = _lib.load()
+    for name, vid in _lib.VARIANTS.items():
+        assert lib.qmha_variant_from_name(name.encode()) == vid
+        assert lib.qmha_variant_name(vid).decode() == name
+    assert lib.qmha_variant_from_name(b"fa_tc_v2") == -1
+    # int8 workspace: 3 int8 tensors + 3 scale arrays
+    ws = lib.qmha_workspace_size(16, 4096, 1024, 16, 2)
+    assert ws >= 3 * 16 * 16 * 4096 * 64 and ws < 3 * 16 * 16 * 4096 * 64 * 1.1
+    assert lib.qmha_workspace_size(2, 256, 128, 2, 0) == 0  # scalar path needs no scratch
+    assert lib.qmha_status_string(1).decode() == "invalid argument"
+
+
+@pytest.mark.parametrize("args,err", [
+    ((1, 100, 128, 2, 2), "N must be a multiple of 32"),
+    ((1, 128, 130, 2, 2), "head size"),
+    ((1, 128, 128, 3, 2), "divisible"),
+    ((1, 128, 128, 2, 7), "unknown variant"),
+    ((0, 128, 128, 2, 2), "positive"),
+])
+def test_invalid_shapes_rejected_before_launch(built, args, err):
+    from quantizedmha_amd import _lib
+    lib = _lib.load()
+    dummy = ctypes.c_void_p(0x1000)  # never dereferenced: checks run first
+    B, N, dm, h, v = args
+    st = lib.qmha_solve_ex(dummy, dummy, dummy, dummy, B, N, dm, h, v, None)
+    assert st in (1, 4)
+    assert err in lib.qmha_last_error().decode()
+    st = lib.qmha_solve_ex(None, dummy, dummy, dummy, 1, 128, 128, 2, 2, None)
+    assert st == 1 and "null" in lib.qmha_last_error().decode()
+
+
+def test_torch_binding_error_behaviour_matches_reference():
+    torch = pytest.importorskip("torch")
+    from quantizedmha_amd import torch_ext
+    q = torch.zeros(64, 32)
+    with pytest.raises(RuntimeError, match="Inputs must be CUDA tensors"):  # torch_ext.cpp:14
+        torch_ext.flash_solve(q, q, q, 32, 4)
+    with pytest.raises(RuntimeError, match="Inputs must be CUDA tensors"):
+        torch_ext.flash_solve(q.double(), q, q, 32, 4)
+
+
+def test_jax_binding_imports_without_jax():
+    from quantizedmha_amd import jax_binding, jax_ext  # noqa: F401
+    try:
+        import jax  # noqa: F401
+    except ImportError:
+        with pytest.raises(ImportError):
+            jax_binding.flash_solve_jax(None, None, None, 32, 4)
+
+
+def test_driver_help_runs_without_gpu(built):
+    exe = os.path.join(ROOT, "quantizedmha_amd", "bin", "qmha_profile")
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert "fa_tc_int8_b" in r.stdout and "--warmup" in r.stdout
+
+
+def test_slot_permutations_are_bijective():
+    """Python restatement of qmha_common.hpp's operand slot maps: each is a permutation of
+    0..31 and matches the MFMA accumulator row map used for P^T."""
+    acc_row = lambda r, h: (r & 3) + 8 * (r >> 2) + 4 * h  # noqa: E731
+    kv_i8 = [acc_row(s & 15, s >> 4) for s in range(32)]
+    assert sorted(kv_i8) == list(range(32))
+    slot_i8 = lambda kv: 16 * ((kv >> 2) & 1) + 4 * (kv >> 3) + (kv & 3)  # noqa: E731
+    assert all(slot_i8(kv_i8[s]) == s for s in range(32))
+    kv_f16 = [16 * (s >> 4) + 4 * ((s >> 3) & 1) + (s & 3) + 8 * ((s >> 2) & 1) for s in range(32)]
+    assert sorted(kv_f16) == list(range(32))
+    # f16 k-step s takes accumulator registers 8s..8s+7 of lane half h
+    for s in range(2):
+        for h in range(2):
+            for e in range(8):
+                assert kv_f16[16 * s + 8 * h + e] == acc_row(8 * s + e, h)
+    assert np.array_equal(np.argsort(kv_f16), [16 * (kv >> 4) + 8 * ((kv >> 2) & 1) + (kv & 3) + 4 * ((kv >> 3) & 1)
+                                               for kv in range(32)])

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Build the MI355X (gfx950) native library, per-variant `solve` libraries and the driver.
+
+    python tools/build.py            # incremental
+    python tools/build.py --clean
+
+Outputs (in-tree, git-ignored, shipped to the GPU box with the snapshot):
+    quantizedmha_amd/lib/libqmha.so                 all C-ABI entry points (include/launchers.h)
+    quantizedmha_amd/lib/libqmha_<variant>.so       `solve` bound to one kernel (reference Makefile KERNEL=)
+    quantizedmha_amd/bin/qmha_profile               HIP C++ host driver (reference drivers/main.cu)
+No CUDA, no hipify, no multi-backend dispatch: hipcc --offload-arch=gfx950 only.
+"""
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "quantizedmha_amd", "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(ROOT, "quantizedmha_amd", "lib")
+BIN = os.path.join(ROOT, "quantizedmha_amd", "bin")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_fa_f32.hip", "qmha_unfused.hip", "qmha_api.cpp"]
+VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3}
+DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
+HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
+
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+                "-Wno-unused-variable", "-Wno-unused-lambda-capture", "-munsafe-fp-atomics"]
+
+
+def newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise SystemExit(f"build failed: {cmd[-1]}")
+    return r
+
+
+def header_deps():
+    deps = [os.path.join(CSRC, h) for h in HEADERS]
+    deps.append(os.path.join(ROOT, "include", "launchers.h"))
+    return deps
+
+
+def compile_one(src, extra=()):
+    out = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o").replace(".cpp", ".o"))
+    if extra:
+        out = out.replace(".o", "_" + "_".join(e.strip("-D").replace("=", "") for e in extra) + ".o")
+    full = os.path.join(CSRC, src)
+    if newer(out, [full] + header_deps() + [__file__]):
+        lang = ["-x", "hip"] if src.endswith(".hip") else []
+        run([HIPCC] + COMMON_FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c"] + lang +
+            [full, "-o", out])
+    return out
+
+
+def build(jobs=8, verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(LIB, exist_ok=True)
+    os.makedirs(BIN, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, KERNEL_SOURCES))
+        shim_objs = {name: ex.submit(compile_one, "qmha_solve_variant.cpp",
+                                     (f"-DQMHA_SOLVE_VARIANT={vid}", f"-DQMHA_SOLVE_NAME={name}"))
+                     for name, vid in VARIANTS.items()}
+        drv_objs = list(ex.map(compile_one, DRIVER_SOURCES))
+        shim_objs = {k: v.result() for k, v in shim_objs.items()}
+    libqmha = os.path.join(LIB, "libqmha.so")
+    if newer(libqmha, objs):
+        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", libqmha] + objs)
+    for name, o in shim_objs.items():
+        out = os.path.join(LIB, f"libqmha_{name}.so")
+        if newer(out, [o, libqmha]):
+            run([HIPCC, "-shared", "-fPIC", "-o", out, o, "-L", LIB, "-lqmha", "-Wl,-rpath,$ORIGIN"])
+    driver = os.path.join(BIN, "qmha_profile")
+    if newer(driver, drv_objs + [libqmha]):
+        run([HIPCC, "-o", driver] + drv_objs + ["-L", LIB, "-lqmha", "-Wl,-rpath,$ORIGIN/../lib"])
+    if verbose:
+        print("built:", libqmha, "+", len(shim_objs), "variant libs +", driver)
+    return libqmha
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=8)
+    a = ap.parse_args()
+    if a.clean:
+        shutil.rmtree(os.path.join(ROOT, "build"), ignore_errors=True)
+        shutil.rmtree(LIB, ignore_errors=True)
+        shutil.rmtree(BIN, ignore_errors=True)
+    build(a.j)
+
+
+if __name__ == "__main__":
+    main()
