@@ -9,7 +9,8 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libqmha.so")
+# QMHA_LIB_PATH: load another build of the same C-ABI (A/B kernel experiments); still no fallback
+LIB_PATH = os.environ.get("QMHA_LIB_PATH") or os.path.join(LIB_DIR, "libqmha.so")
 
 VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3}
 DEFAULT_KERNEL = "fa_tc_int8_b"

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -162,7 +163,7 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
     switch (variant) {
         case QMHA_FA_TC_INT8_B: {
             qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
-            QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, B, N, h, D, d_model, stream), "quant_int8 launch");
+            QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, 1, B, N, h, D, d_model, stream), "quant_int8 launch");
             rec.has_pre = true;
             if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
             QMHA_HIP_TRY(qmha::launch_fa_int8_main(w, O, B, N, h, D, d_model, stream), "fa_int8 launch");
@@ -199,6 +200,21 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
 }
 
 }  // namespace
+
+int qmha::tune_config(const char* env_name) {
+    static std::mutex mu;
+    static std::map<std::string, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(env_name);
+    if (it != cache.end()) return it->second;
+    int v = 0;
+    if (const char* e = std::getenv(env_name)) {
+        int w = 0, sg = 0;
+        if (std::sscanf(e, "%dx%d", &w, &sg) == 2 && w > 0 && w < 10 && sg > 0 && sg < 10) v = w * 10 + sg;
+    }
+    cache[env_name] = v;
+    return v;
+}
 
 extern "C" {
 
@@ -251,14 +267,18 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
     st = get_workspace(need, (hipStream_t)stream, &ws);
     if (st != QMHA_OK) return st;
     qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
+    void* vout = w.Vh;
+    int v_mode = 1;
     if (layout == 0) {
         w.Qi = Xi;
         w.sQ = scales;
     } else {
-        w.Vt = Xi;
+        vout = Xi;
+        v_mode = 0;
         w.sV = scales;
     }
-    QMHA_HIP_TRY(qmha::launch_quant_int8(X, X, X, w, B, N, h, D, d_model, (hipStream_t)stream), "quant_int8 launch");
+    QMHA_HIP_TRY(qmha::launch_quant_int8(X, X, X, w, vout, v_mode, B, N, h, D, d_model, (hipStream_t)stream),
+                 "quant_int8 launch");
     return QMHA_OK;
 }
 
@@ -275,7 +295,7 @@ int qmha_debug_qk_int32(const float* Q, const float* K, int N, int d_model, int 
     st = get_workspace(need, nullptr, &ws);
     if (st != QMHA_OK) return st;
     qmha::Int8Workspace w = qmha::int8_carve(ws, 1, N, h, D);
-    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, Q, w, 1, N, h, D, d_model, nullptr), "quant_int8 launch");
+    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, Q, w, w.Vh, 1, 1, N, h, D, d_model, nullptr), "quant_int8 launch");
     QMHA_HIP_TRY(qmha::launch_debug_qk_int32(w, N, D, head, S, nullptr), "debug_qk launch");
     QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
     return QMHA_OK;

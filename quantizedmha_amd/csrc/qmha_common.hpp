@@ -18,6 +18,18 @@
 
 #define QMHA_GROUP 32
 
+// ISA inspection builds (-DQMHA_ISA_MARKS): an s_nop 15 fence around a code region so
+// tools/isa.py can cut it out of the disassembly.  Empty in every real build.
+#ifdef QMHA_ISA_MARKS
+#define QMHA_ISA_MARK() asm volatile("s_nop 15" ::: "memory")
+#else
+#define QMHA_ISA_MARK() ((void)0)
+#endif
+
+// address-space pointer types for __builtin_amdgcn_global_load_lds (LDS-DMA)
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
@@ -80,6 +92,22 @@ __device__ __forceinline__ float half_max32(float x) {
     return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
 }
 
+// Max over the 32 lanes of each half for NON-NEGATIVE floats, on the bit patterns (integer
+// max orders non-negative IEEE floats; avoids the NaN-canonicalising v_max_f32 pairs).
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov_i(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float half_max32_nonneg(float xf) {
+    int x = __float_as_int(xf);
+    x = max(x, dpp_mov_i<0xB1>(x));
+    x = max(x, dpp_mov_i<0x4E>(x));
+    x = max(x, dpp_mov_i<0x141>(x));
+    x = max(x, dpp_mov_i<0x140>(x));
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __int_as_float(max((int)r[0], (int)r[1]));
+}
+
 // Max over all 64 lanes.
 __device__ __forceinline__ float wave_max64(float x) { return half_swap_max(half_max32(x)); }
 
@@ -92,6 +120,32 @@ __device__ __forceinline__ float qmha_scale_from_absmax(float absmax) {
 __device__ __forceinline__ int qmha_quant_i8(float v, float inv) {
     int q = __float2int_rn(v * inv);
     return q < -128 ? -128 : (q > 127 ? 127 : q);
+}
+
+// x / 127 and 1 / x with two fma corrections (Markstein): the correctly rounded quotient
+// except in rare double-rounding cases, in 3 VALU ops instead of the ~10-op IEEE sequence.
+// Valid for normal, finite x (the P-tile maxima and scales they are used on).
+__device__ __forceinline__ float div127_fast(float x) {
+    const float r = 1.0f / 127.0f;
+    const float q = x * r;
+    return fmaf(fmaf(-q, 127.0f, x), r, q);
+}
+__device__ __forceinline__ float rcp_fast(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(fmaf(-x, r, 1.0f), r, r);
+}
+
+// Balanced-tree reductions of 16 register values (independent chains for ILP).
+__device__ __forceinline__ int tree_max16_i(const v16i& s) {
+    int a = max(max(s[0], s[1]), s[2]), b = max(max(s[3], s[4]), s[5]);
+    int c = max(max(s[6], s[7]), s[8]), d = max(max(s[9], s[10]), s[11]);
+    int e = max(max(s[12], s[13]), s[14]);
+    return max(max(max(a, b), max(c, d)), max(e, (int)s[15]));
+}
+__device__ __forceinline__ float tree_sum16(const float* p) {
+    float a = (p[0] + p[1]) + (p[2] + p[3]), b = (p[4] + p[5]) + (p[6] + p[7]);
+    float c = (p[8] + p[9]) + (p[10] + p[11]), d = (p[12] + p[13]) + (p[14] + p[15]);
+    return (a + b) + (c + d);
 }
 
 // Round-half-even of a non-negative x < 2^22 into the low mantissa bits:

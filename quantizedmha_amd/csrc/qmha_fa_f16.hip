@@ -79,10 +79,11 @@ __device__ __forceinline__ int chunk_swz_h(int row) {
     return (row / rpb) & (RB / 16 - 1);
 }
 
-template <int D, int WAVES, int SG>
+template <int D, int WAVES, int SG = 2>
 __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
     const _Float16* __restrict__ Qh, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    static_assert(SG == 2, "the stage is processed as one interleaved pair of tiles");
     constexpr int KS = D / 16;   // QK k-steps (K = 16)
     constexpr int MB = D / 32;   // PV d-blocks
     constexpr int RB = 2 * D;    // K row bytes
@@ -155,6 +156,58 @@ __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
         }
     };
 
+    // S^T = K Q^T (f32 accumulate) of tile gi of the stage in LDS
+    auto qk = [&](const char* L, int gi) {
+        v16f s = {};
+        const int krow = gi * 32 + col;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
+            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
+        }
+        return s;
+    };
+    auto rowmax = [&](const v16f& s) {
+        float a = fmaxf(fmaxf(s[0], s[1]), s[2]), b = fmaxf(fmaxf(s[3], s[4]), s[5]);
+        float c = fmaxf(fmaxf(s[6], s[7]), s[8]), d = fmaxf(fmaxf(s[9], s[10]), s[11]);
+        float e = fmaxf(fmaxf(s[12], s[13]), s[14]);
+        return half_swap_max(fmaxf(fmaxf(fmaxf(a, b), fmaxf(c, d)), fmaxf(e, s[15])));
+    };
+    // P = half(exp(s - m)) as the two k-step operands; rs = sum of the fp32 p (fa_tc_v1a.cu:169-174)
+    auto ptile = [&](const v16f& s, float m, v8h* pop, float& rs) {
+        float p[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m));
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const v2h h2 = __builtin_convertvector((v2f{p[r], p[r + 1]}), v2h);  // v_cvt_pk_f16_f32 (RNE)
+            pop[r >> 3][r & 7] = h2[0];
+            pop[r >> 3][(r & 7) + 1] = h2[1];
+        }
+        rs = tree_sum16(p);
+    };
+    auto rescale = [&](float a) {
+        if (__builtin_amdgcn_ballot_w64(a != 1.0f)) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[m][r] *= a;
+        }
+    };
+    // O^T += V^T P^T with the fp32 accumulator as the MFMA C operand (fa_tc_v1a.cu:218)
+    auto pv = [&](const char* L, int gi, const v8h* pop) {
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            const int d = 32 * m + col;
+            const char* vr = L + STAGE_BYTES + gi * 64 * D + d * 64;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
+            }
+        }
+    };
+
     gload(0);
     lstore(0, 0);
     __syncthreads();
@@ -162,57 +215,40 @@ __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
         const int buf = st & 1;
         if (st + 1 < nst) gload(st + 1);
         if (active) {
-            const int g0 = st * SG;
-            const int ngr = min(SG, G - g0);
+            const int t0 = st * SG;
             const char* L = lds[buf];
-#pragma unroll
-            for (int gi = 0; gi < SG; ++gi) {
-                if (gi < ngr) {
-                    v16f s = {};
-                    const int krow = gi * 32 + col;
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
-                        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
-                    }
-                    float mx = s[0];
-#pragma unroll
-                    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
-                    mx = half_swap_max(mx);
-                    const float m_new = fmaxf(m_run, mx * c_log2);
-                    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-                    float rs = 0.0f;
-                    v8h pop[2];
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_new));
-                        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c_log2, -m_new));
-                        rs += p0;
-                        rs += p1;
-                        const v2h h2 = __builtin_convertvector((v2f{p0, p1}), v2h);  // v_cvt_pk_f16_f32 (RNE)
-                        pop[r >> 3][r & 7] = h2[0];
-                        pop[r >> 3][(r & 7) + 1] = h2[1];
-                    }
-                    rs = half_swap_add(rs);
-                    l_run = fmaf(alpha, l_run, rs);  // fa_tc_v1a.cu:198
-                    m_run = m_new;
-                    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
-#pragma unroll
-                        for (int m = 0; m < MB; ++m)
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) o[m][r] *= alpha;
-                    }
-#pragma unroll
-                    for (int m = 0; m < MB; ++m) {
-                        const int d = 32 * m + col;
-                        const char* vr = L + STAGE_BYTES + gi * 64 * D + d * 64;
-#pragma unroll
-                        for (int ks = 0; ks < 2; ++ks) {
-                            const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
-                            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
-                        }
-                    }
-                }
+            if (t0 + 1 < G) {
+                // interleaved pair; the running max is chained per 32-key tile (:286-303)
+                const v16f s0 = qk(L, 0);
+                const v16f s1 = qk(L, 1);
+                const float m1 = fmaxf(m_run, rowmax(s0) * c_log2);
+                const float m2 = fmaxf(m1, rowmax(s1) * c_log2);
+                const float a1 = __builtin_amdgcn_exp2f(m_run - m1);  // :195
+                const float a2 = __builtin_amdgcn_exp2f(m1 - m2);
+                v8h p0[2], p1[2];
+                float rs0, rs1;
+                ptile(s0, m1, p0, rs0);
+                ptile(s1, m2, p1, rs1);
+                rs0 = half_swap_add(rs0);
+                rs1 = half_swap_add(rs1);
+                l_run = fmaf(a2, fmaf(a1, l_run, rs0), rs1);  // :198 twice
+                m_run = m2;
+                rescale(a1);  // :207
+                pv(L, 0, p0);
+                rescale(a2);
+                pv(L, 1, p1);
+            } else {
+                const v16f s0 = qk(L, 0);
+                const float m1 = fmaxf(m_run, rowmax(s0) * c_log2);
+                const float a1 = __builtin_amdgcn_exp2f(m_run - m1);
+                v8h p0[2];
+                float rs0;
+                ptile(s0, m1, p0, rs0);
+                rs0 = half_swap_add(rs0);
+                l_run = fmaf(a1, l_run, rs0);
+                m_run = m1;
+                rescale(a1);
+                pv(L, 0, p0);
             }
         }
         if (st + 1 < nst) lstore(buf ^ 1, st + 1);
@@ -266,15 +302,27 @@ hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, co
     }
 }
 
-template <int D>
-static hipError_t fa_f16_d(const F16Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
-    constexpr int WAVES = 4, SG = 2;
+template <int D, int WAVES, int SG>
+static hipError_t fa_f16_launch(const F16Workspace& w, float* O, int B, int N, int H, int d_model,
+                                hipStream_t stream) {
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;  // fa_tc_v1a.cu:421
     hipLaunchKernelGGL((qmha_fa_f16_kernel<D, WAVES, SG>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qh, w.Kh,
                        w.Vt, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
+}
+
+template <int D>
+static hipError_t fa_f16_d(const F16Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
+    if constexpr (D == 64) {
+        switch (tune_config("QMHA_F16_CFG")) {
+            case 82: return fa_f16_launch<D, 8, 2>(w, O, B, N, H, d_model, stream);
+            case 22: return fa_f16_launch<D, 2, 2>(w, O, B, N, H, d_model, stream);
+            default: break;
+        }
+    }
+    return fa_f16_launch<D, 4, 2>(w, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,

@@ -10,19 +10,24 @@ namespace qmha {
 
 inline constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Tuning knob for benchmarking kernel geometries: env var "<waves>x<stages>" (e.g. "8x2")
+// read once per variable; returns waves*10+stages, or 0 (= built-in default).
+int tune_config(const char* env_name);
+
 // ---- INT8 (fa_tc_int8_b) ---------------------------------------------------------------
 struct Int8Workspace {
     int8_t* Qi;  // [B*H][N][D]
     int8_t* Ki;  // [B*H][N][D]
-    int8_t* Vt;  // [B*H][N/32][D][32]  (i8 operand slot order, qmha_common.hpp)
+    _Float16* Vh;  // [B*H][N/32][D][32]  quantised V as f16 integers (f16 operand slot order)
     float* sQ;   // [B*H][N/32]
     float* sK;
     float* sV;
 };
 size_t int8_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D);
-hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
-                             int H, int D, int d_model, hipStream_t stream);
+// v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
+hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
+                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream);
 hipError_t launch_fa_int8_main(const Int8Workspace& w, float* O, int B, int N, int H, int D, int d_model,
                                hipStream_t stream);
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream);

@@ -66,9 +66,9 @@ def test_host_side_queries(built):
         assert lib.qmha_variant_from_name(name.encode()) == vid
         assert lib.qmha_variant_name(vid).decode() == name
     assert lib.qmha_variant_from_name(b"fa_tc_v2") == -1
-    # int8 workspace: 3 int8 tensors + 3 scale arrays
+    # int8 workspace: int8 Q and K, V as f16-valued integers (main-kernel operand), 3 scale arrays
     ws = lib.qmha_workspace_size(16, 4096, 1024, 16, 2)
-    assert ws >= 3 * 16 * 16 * 4096 * 64 and ws < 3 * 16 * 16 * 4096 * 64 * 1.1
+    assert ws >= 4 * 16 * 16 * 4096 * 64 and ws < 4 * 16 * 16 * 4096 * 64 * 1.1
     assert lib.qmha_workspace_size(2, 256, 128, 2, 0) == 0  # scalar path needs no scratch
     assert lib.qmha_status_string(1).decode() == "invalid argument"
 

@@ -23,7 +23,13 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-INT8_TOL_ORACLE = 3e-4
+# int8 vs oracle: the GPU's exp2 and the oracle's expf differ in the last ulp, which can move
+# p/sP across a .5 rounding boundary and change one Pi by 1.  One such flip moves O by
+# sP*sV*|Vi|/l (up to ~1e-3 at N=128), so the int8 check is statistical: every element within
+# INT8_TOL_ORACLE, and all but INT8_FLIP_FRAC of the elements within INT8_TOL_TIGHT.
+INT8_TOL_ORACLE = 2e-3
+INT8_TOL_TIGHT = 5e-5
+INT8_FLIP_FRAC = 2e-3
 TOL_ORACLE = {"fa_tc_int8_b": INT8_TOL_ORACLE, "fa_tc_v1a": 2e-4, "fa": 1e-5, "unfused": 1e-5}
 TOL_GOLDEN = {"fa_tc_int8_b": 5e-3, "fa_tc_v1a": 1e-3, "fa": 1e-5, "unfused": 1e-5}
 VARIANTS = list(TOL_ORACLE)
@@ -40,6 +46,15 @@ def dev():
 
 def oracle_for(oracle_mod, variant):
     return oracle_mod.ORACLE_BY_VARIANT[variant]
+
+
+def assert_parity(variant, out, ref, scale=1.0):
+    err = np.abs(np.asarray(out, np.float64) - np.asarray(ref, np.float64))
+    assert np.isfinite(out).all()
+    assert err.max() <= TOL_ORACLE[variant] * scale, (variant, float(err.max()))
+    if variant == "fa_tc_int8_b":
+        frac = float((err > INT8_TOL_TIGHT).mean())
+        assert frac <= INT8_FLIP_FRAC, (frac, float(err.max()))
 
 
 def run(variant, Q, K, V, d_model, h, dev):
@@ -101,10 +116,9 @@ def test_variant_vs_reference_golden(dev, oracle_mod, variant, case):
     out = run(variant, Q, K, V, dm, h, dev)
     assert np.isfinite(out).all()
     ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
-    e_or = np.abs(out - ref).max()
+    assert_parity(variant, out, ref)
     e_gold = np.abs(out - O).max()
-    assert e_or <= TOL_ORACLE[variant], (e_or, e_gold)
-    assert e_gold <= TOL_GOLDEN[variant], (e_or, e_gold)
+    assert e_gold <= TOL_GOLDEN[variant], e_gold
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -119,8 +133,7 @@ def test_variant_vs_oracle_random(dev, oracle_mod, variant, B, N, d_model, h, di
     Q, K, V = rand_inputs(10 + N + B, B, N, d_model, dist)
     out = run(variant, Q, K, V, d_model, h, dev)
     ref = oracle_for(oracle_mod, variant)(Q, K, V, d_model, h)
-    err = np.abs(out - ref).max()
-    assert err <= TOL_ORACLE[variant], err
+    assert_parity(variant, out, ref)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -140,14 +153,14 @@ def test_edge_values(dev, oracle_mod, variant):
     V = (rng.standard_normal((N, dm))).astype(np.float32)
     out = run(variant, Q, K, V, dm, h, dev)
     ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
-    assert np.abs(out - ref).max() <= TOL_ORACLE[variant]
+    assert_parity(variant, out, ref)
     # a spike: one key far above the rest forces a large running-max jump mid-sequence
     Q = (rng.standard_normal((N, dm)) * 0.5).astype(np.float32)
     K = (rng.standard_normal((N, dm)) * 0.5).astype(np.float32)
     K[77] = Q[3] * 8
     out = run(variant, Q, K, V, dm, h, dev)
     ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
-    assert np.abs(out - ref).max() <= TOL_ORACLE[variant] * 4
+    assert_parity(variant, out, ref, scale=4)
 
 
 def test_deterministic(dev):
@@ -169,7 +182,7 @@ def test_c_abi_solve_per_variant_libraries(dev, oracle_mod):
         out = torch.empty_like(tq)
         lib.solve(tq.data_ptr(), tk.data_ptr(), tv.data_ptr(), out.data_ptr(), N, dm, h)
         ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
-        assert np.abs(out.cpu().numpy() - ref).max() <= TOL_ORACLE[variant], variant
+        assert_parity(variant, out.cpu().numpy(), ref)
 
 
 def test_jax_ext_raw_pointer_entry(dev, oracle_mod):
@@ -201,7 +214,7 @@ def test_full_baseline_config_sampled_heads(dev, oracle_mod):
         cols = slice(k * d, (k + 1) * d)
         q, kk, v = (x[b, :, cols].cpu().numpy() for x in (Q, K, V))
         ref = oracle_mod.fa_int8(q, kk, v, d, 1)
-        assert np.abs(out[b, :, cols].cpu().numpy() - ref).max() <= INT8_TOL_ORACLE
+        assert_parity("fa_tc_int8_b", out[b, :, cols].cpu().numpy(), ref)
 
 
 def test_driver_binary_end_to_end(dev, tmp_path):

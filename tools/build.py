@@ -31,7 +31,10 @@ DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
 HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-                "-Wno-unused-variable", "-Wno-unused-lambda-capture", "-munsafe-fp-atomics"]
+                "-Wno-unused-variable", "-Wno-unused-lambda-capture", "-munsafe-fp-atomics",
+                "-mllvm", "-amdgpu-mfma-vgpr-form"]
+# profiling builds only, e.g. QMHA_EXTRA_FLAGS=-DQMHA_ABLATION (rebuild with --clean)
+COMMON_FLAGS += os.environ.get("QMHA_EXTRA_FLAGS", "").split()
 
 
 def newer(target, deps):
