@@ -57,7 +57,9 @@ def main():
         if "WRITE_SIZE" in c:
             der["hbm_write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
-            der["mfma_busy_pct"] = 100 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] * 1024)
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy cycles over all 1024 SIMDs
+            der["mfma_busy_pct"] = 100 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            der["effective_clock_ghz_x_ms"] = c["GRBM_GUI_ACTIVE"] / 8 / 1e6
         if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
             der["valu_active_per_wave_cycle"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
         for n, v in der.items():
