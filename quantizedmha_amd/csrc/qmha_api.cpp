@@ -210,7 +210,11 @@ int qmha::tune_config(const char* env_name) {
     int v = 0;
     if (const char* e = std::getenv(env_name)) {
         int w = 0, sg = 0;
-        if (std::sscanf(e, "%dx%d", &w, &sg) == 2 && w > 0 && w < 10 && sg > 0 && sg < 10) v = w * 10 + sg;
+        if (std::sscanf(e, "%dx%d", &w, &sg) == 2 && w > 0 && w < 10 && sg > 0 && sg < 10) {
+            v = w * 10 + sg;  // "WAVESxSG"
+        } else if (std::sscanf(e, "%d", &w) == 1 && w > 0) {
+            v = w;  // a kernel-specific numeric geometry code
+        }
     }
     cache[env_name] = v;
     return v;

@@ -18,6 +18,17 @@
 
 #define QMHA_GROUP 32
 
+// MFMA accumulators in AGPRs.  On gfx950 a VALU stream overlaps another wave's MFMA stream
+// only when the MFMA's C/D operands live in AGPRs (tools/ubench/mfma_coexec.hip: v_fma_f32 beside
+// 32x32x16 MFMAs 0.35 ms with AGPR accumulators vs 0.52 ms with VGPR ones = no overlap).  The
+// compiler selects the AGPR form only for functions that may use AGPRs, which this empty
+// clobber declares; the build drops -amdgpu-mfma-vgpr-form when QMHA_MFMA_AGPR is set.
+#ifdef QMHA_MFMA_AGPR
+#define QMHA_ENABLE_AGPR_MFMA() asm volatile("" ::: "a0")
+#else
+#define QMHA_ENABLE_AGPR_MFMA() ((void)0)
+#endif
+
 // ISA inspection builds (-DQMHA_ISA_MARKS): an s_nop 15 fence around a code region so
 // tools/isa.py can cut it out of the disassembly.  Empty in every real build.
 #ifdef QMHA_ISA_MARKS

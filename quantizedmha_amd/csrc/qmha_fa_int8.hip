@@ -30,6 +30,7 @@
 #include "qmha_kernels.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace qmha {
 
@@ -145,59 +146,77 @@ __device__ __forceinline__ int chunk_swz(int row) {
 
 // ---------------------------------------------------------------------------------------
 // Main kernel.
+//
+// One workgroup = WAVES waves; each wave owns QPW 32-row Q groups (= Q quantisation groups)
+// of one head and sweeps all KV groups of that head.  Per 32-key tile and Q group:
+//   S^T = K Q^T            v_mfma_i32_32x32x32_i8 (int32, exact; K operand shared by the
+//                          wave's Q groups)
+//   online softmax         lane-local per query (swapped product), m0 = 0
+//   P tile scale sP        max over the 32x32 tile (DPP + permlane16)
+//   Pi = rint(p / sP)      magic-number RNE, packed to f16
+//   O^T += V^T P^T         v_mfma_f32_32x32x16_f16 on exact f16 integers (= the int32 product)
+// FL (build-time flags):
+//   FL_MAGIC    the Q@K^T chain starts from the bits of 1.5*2^23, so every int32 accumulator lane
+//               reads as the float 1.5*2^23 + S (exact: |S| <= 2^21 for d <= 128); one packed
+//               subtract recovers float(S) for two scores (replaces two v_cvt_f32_i32)
+//   FL_PREFETCH Q@K^T of tile t+1 issued before the softmax of tile t (QPW == 1)
+//   FL_LB2      register budget of 2 waves per SIMD (256 VGPRs) instead of 4 (128)
+// ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
+//   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-// ABL: ablation bitmask for profiling builds only (0 in production; results are wrong
-// otherwise): 1 = no exp2 on P, 2 = no P@V MFMA, 4 = no Q@K^T MFMA, 8 = no P-tile max
-// reduction, 16 = no compute at all (K/V staging and barriers only), 64 = no K/V staging and
-// no barriers (every stage recomputes on LDS buffer 0), 32 = phase-separated softmax,
-// 128 = magic-offset Q@K^T accumulator + packed score/sum arithmetic + anchored l,
-// 256 = no Q@K^T prefetch across tiles, 512 = 2 waves/SIMD register budget.
-template <int D, int WAVES, int SG, int ABL = 0>
-// 2nd launch bound = minimum waves per SIMD: 4 caps the allocation at 128 VGPRs, so four
-// waves share each SIMD (the VALU-bound softmax needs them to fill the issue slots).
-__global__ __launch_bounds__(WAVES * 64, (ABL & 512) ? 2 : 4) void qmha_fa_int8_kernel(
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4 };
+
+template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
+__global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
     const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sQ, const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     constexpr int KS = D / 32;                    // i8 MFMA k-steps (QK) and d-blocks (PV)
     constexpr int KBYTES = SG * 32 * D;           // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;       // V f16 per stage
-    constexpr int NT = WAVES * 64;
     constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    constexpr bool MAGIC = FL & FL_MAGIC;
     static_assert(KCH % 64 == 0 && VCH % 64 == 0, "a stage is whole KiB LDS-DMA pieces");
     static_assert((KCH / SG) % 64 == 0, "a KV group is whole KiB pieces (D >= 32)");
+    static_assert(!(FL & FL_PREFETCH) || QPW == 1, "prefetch pipeline is for one Q group per wave");
     __shared__ __attribute__((aligned(16))) int8_t lds[2][KBYTES + VBYTES];
 
+    QMHA_ENABLE_AGPR_MFMA();
     const int G = N / QMHA_GROUP;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = wg / nqb, qb = wg % nqb;
     const int b = bh / H, k = bh % H;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int qg = qb * WAVES + wave;
-    const bool active = qg < G;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int half = lane >> 5, col = lane & 31;
 
-    v4i qop[KS];
-    float cq = 0.0f;
-    if (active) {
-        const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
+    // per Q group state
+    v4i qop[QPW][KS];
+    float cq[QPW];
+    v16f o[QPW][KS];
+    float m_run[QPW], l_run[QPW], anchor[QPW];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) qop[s] = *reinterpret_cast<const v4i*>(qp + 32 * s);
-        cq = sQ[(size_t)bh * G + qg] * c_log2;
-    } else {
+    for (int j = 0; j < QPW; ++j) {
+        const int qg = (qb * WAVES + wave) * QPW + j;
+        if (qg < G) {  // wave-uniform
+            const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) qop[s] = v4i{0, 0, 0, 0};
+            for (int s = 0; s < KS; ++s) qop[j][s] = *reinterpret_cast<const v4i*>(qp + 32 * s);
+            cq[j] = sQ[(size_t)bh * G + qg] * c_log2;
+        } else {  // padding group: computes on a zero Q, never stored
+#pragma unroll
+            for (int s = 0; s < KS; ++s) qop[j][s] = v4i{0, 0, 0, 0};
+            cq[j] = 0.0f;
+        }
+#pragma unroll
+        for (int m = 0; m < KS; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[j][m][r] = 0.0f;
+        m_run[j] = 0.0f;   // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
+        l_run[j] = 0.0f;   // anchored: l * 2^(anchor - m)
+        anchor[j] = 0.0f;  // o = O * 2^(m - anchor), anchor <= m
     }
-
-    v16f o[KS];
-#pragma unroll
-    for (int m = 0; m < KS; ++m)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[m][r] = 0.0f;
-    float m_run = 0.0f;  // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
-    float l_run = 0.0f;
-    float anchor = 0.0f;  // o = O * 2^(m_run - anchor), anchor <= m_run
+    const bool any_active = (qb * WAVES + wave) * QPW < G;  // wave-uniform
 
     const int8_t* kbase = Ki + (size_t)bh * N * D;
     const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
@@ -214,17 +233,17 @@ __global__ __launch_bounds__(WAVES * 64, (ABL & 512) ? 2 : 4) void qmha_fa_int8_
         const char* vsrc = vbase + (size_t)st * VBYTES;
         int8_t* L = lds[buf];
 #pragma unroll
-        for (int j = 0; j < (KCH / 64 + WAVES - 1) / WAVES; ++j) {
-            const int inst = wave + j * WAVES;  // KiB piece of the K stage
+        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;  // KiB piece of the K stage
             if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
-                const int idx = inst * 64 + lane;              // LDS chunk this lane fills
+                const int idx = inst * 64 + lane;  // LDS chunk this lane fills
                 const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
                 __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * D + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
             }
         }
 #pragma unroll
-        for (int j = 0; j < (VCH / 64 + WAVES - 1) / WAVES; ++j) {
-            const int inst = wave + j * WAVES;
+        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
             if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
                 const int idx = inst * 64 + lane;
                 const int grp = idx / (4 * D), w = idx % (4 * D);
@@ -234,122 +253,99 @@ __global__ __launch_bounds__(WAVES * 64, (ABL & 512) ? 2 : 4) void qmha_fa_int8_
             }
         }
     };
-    // S^T = K Q^T (int32) of tile gi of the stage in LDS
-    // ABL&128: the Q@K^T chain starts from the bit pattern of 1.5*2^23, so each int32 lane of
-    // the result reads as the float 1.5*2^23 + S (exact: |S| <= 2^21) -- one packed subtract
-    // then yields float(S) for two scores, replacing two v_cvt_f32_i32.
+
     v16i magic_blk;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) magic_blk[r] = 0x4B400000;
-    asm volatile("" : "+v"(magic_blk));  // keep it resident, not rematerialised per tile
-    auto qk = [&](const int8_t* L, int gi) {
-        v16i s = (ABL & 128) ? magic_blk : v16i{};
+    for (int r = 0; r < 16; ++r) magic_blk[r] = MAGIC ? 0x4B400000 : 0;
+    if constexpr (MAGIC) asm volatile("" : "+v"(magic_blk));  // resident, not rematerialised per tile
+
+    // S^T = K Q^T of tile gi of the stage in LDS, for every Q group of the wave
+    auto qk = [&](const int8_t* L, int gi, v16i (&s)[QPW]) {
         const int krow = gi * 32 + col;
+#pragma unroll
+        for (int j = 0; j < QPW; ++j) s[j] = MAGIC ? magic_blk : v16i{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const v4i kop = *reinterpret_cast<const v4i*>(L + krow * D + 16 * ((2 * ks + half) ^ chunk_swz<D>(krow)));
-            if constexpr (ABL & 4) {
-                asm volatile("" : "+v"(s) : "v"(kop), "v"(qop[ks]));
-            } else {
-                s = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop, qop[ks], s, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < QPW; ++j) {
+                if constexpr (ABL & 4) {  // opaque result, no instruction
+                    asm volatile("" : "=v"(s[j]) : "v"(kop), "v"(qop[j][ks]));
+                } else {
+                    s[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop, qop[j][ks], s[j], 0, 0, 0);
+                }
             }
         }
-        return s;
     };
-    // one tile: online softmax (fa_tc_int8_b.cu:281-346), P quantisation (:359), P@V (:366-371)
-    auto tile = [&](const int8_t* L, int gi, int t, const v16i& s) {
-        const float c = cq * skb[t];  // sQ*sK*log2(e)/sqrt(d) > 0
-        const float mx = (ABL & 128) ? __int_as_float(half_swap_max_i(tree_max16_i(s))) - QMHA_MAGIC_RNE
-                                     : (float)half_swap_max_i(tree_max16_i(s));
-        const float m_new = fmaxf(m_run, mx * c);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        float p[16];
-        v8h pop[2];
-        float sp, invp;
-        // tile max of p = exp(tile row max - m), then the max over the 32 query rows
-        auto pscale = [&]() {
-            const float pmax = (ABL & 8) ? fmaf(mx, c, -m_new) : half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
-            sp = fmaxf(div127_fast(pmax), 1e-8f);  // sP = max(absmax/127, 1e-8)
-            invp = rcp_fast(sp);                   // 1/sP
-        };
-        if constexpr (ABL & 128) {
-            pscale();
-            const v2f mg = {QMHA_MAGIC_RNE, QMHA_MAGIC_RNE}, cc = {c, c}, nm = {-m_new, -m_new};
+
+    // one tile for every Q group: online softmax (fa_tc_int8_b.cu:281-346), P quantisation
+    // (:359), P@V (:366-371)
+    auto tile = [&](const int8_t* L, int gi, int t, v16i (&s)[QPW]) {
+        const float skt = skb[t], svt = svb[t];
+        float p[QPW][16];
+        v8h pop[QPW][2];
+        float scale[QPW];
 #pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-                v2f x = v2f{__int_as_float(s[r]), __int_as_float(s[r + 1])} - mg;  // float(S), exact
-                x = __builtin_elementwise_fma(x, cc, nm);
-                p[r] = __builtin_amdgcn_exp2f(x[0]);
-                p[r + 1] = __builtin_amdgcn_exp2f(x[1]);
-            }
-        } else if constexpr (ABL & 32) {
-            // phase-separated: every phase is 16 independent instructions
-#pragma unroll
-            for (int r = 0; r < 16; ++r) p[r] = (float)s[r];
-            __builtin_amdgcn_sched_barrier(0);
-            pscale();
-#pragma unroll
-            for (int r = 0; r < 16; ++r) p[r] = fmaf(p[r], c, -m_new);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if constexpr (!(ABL & 1)) p[r] = __builtin_amdgcn_exp2f(p[r]);
-            __builtin_amdgcn_sched_barrier(0);
-        } else {
-            pscale();
+        for (int j = 0; j < QPW; ++j) {
+            const float c = cq[j] * skt;  // sQ*sK*log2(e)/sqrt(d) >= 0
+            const int mxi = half_swap_max_i(tree_max16_i(s[j]));
+            const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
+            const float m_new = fmaxf(m_run[j], mx * c);
+            // tile max of p = exp(row max - m), then the max over the 32 query rows (:359)
+            const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
+            const float sp = fmaxf(div127_fast(pmax), 1e-8f);  // sP = max(absmax/127, 1e-8)
+            const float invp = rcp_fast(sp);                   // 1/sP
+            // scores -> p = exp2(S*c - m).  Scalar fp32 ops throughout: on gfx950 v_pk_*_f32 issue
+            // at half the rate of v_fma/v_add (no throughput gain) and never overlap the MFMAs.
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                p[r] = fmaf((float)s[r], c, -m_new);
-                if constexpr (!(ABL & 1)) p[r] = __builtin_amdgcn_exp2f(p[r]);
+                const float sv = MAGIC ? __int_as_float(s[j][r]) - QMHA_MAGIC_RNE : (float)s[j][r];
+                const float x = fmaf(sv, c, -m_new);
+                p[j][r] = (ABL & 1) ? x : __builtin_amdgcn_exp2f(x);
             }
-        }
+            // Pi = rint(p/sP) as exact f16 integers (0..127)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            // Pi = rint(p/sP) as an exact f16 integer (0..127)
-            const float q0 = fmaf(p[r], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
-            const float q1 = fmaf(p[r + 1], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
-            const v2h h2 = __builtin_convertvector((v2f{q0, q1}), v2h);
-            pop[r >> 3][r & 7] = h2[0];
-            pop[r >> 3][(r & 7) + 1] = h2[1];
+            for (int r = 0; r < 16; r += 2) {
+                const float q0 = fmaf(p[j][r], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+                const float q1 = fmaf(p[j][r + 1], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+                const v2h h2 = __builtin_convertvector((v2f{q0, q1}), v2h);
+                pop[j][r >> 3][r & 7] = h2[0];
+                pop[j][r >> 3][(r & 7) + 1] = h2[1];
+            }
+            // row sum of the unquantised p (:336) + the other lane half
+            const float rs = half_swap_add(tree_sum16(p[j]));
+            // Anchored running state: o = O * 2^(m - anchor), l_run = l * 2^(m - anchor).  The
+            // reference's O = alpha*O + T*sP*sV and l = alpha*l + rowsum (:336,:344,:369-371)
+            // become o += T*sP*sV*2^(m_t - anchor) and l_run += rowsum*2^(m_t - anchor):
+            // mathematically identical, no per-tile pass over O and no alpha.
+            const float e = __builtin_amdgcn_exp2f(m_new - anchor[j]);
+            l_run[j] = fmaf(rs, e, l_run[j]);
+            m_run[j] = m_new;
+            scale[j] = sp * svt * e;
         }
-        float rs;
-        if constexpr (ABL & 128) {
-            // pairwise tree in packed form (p[r], p[r+1] are adjacent registers)
-            v2f t0 = v2f{p[0], p[1]} + v2f{p[2], p[3]}, t1 = v2f{p[4], p[5]} + v2f{p[6], p[7]};
-            v2f t2 = v2f{p[8], p[9]} + v2f{p[10], p[11]}, t3 = v2f{p[12], p[13]} + v2f{p[14], p[15]};
-            const v2f u = (t0 + t1) + (t2 + t3);
-            rs = half_swap_add(u[0] + u[1]);
-        } else {
-            rs = half_swap_add(tree_sum16(p));
-        }
-        const float e_anchor = __builtin_amdgcn_exp2f(m_new - anchor);
-        if constexpr (ABL & 128) {
-            l_run = fmaf(rs, e_anchor, l_run);  // anchored l: l_run holds l * 2^(anchor - m)
-        } else {
-            l_run = fmaf(alpha, l_run, rs);  // :336
-        }
-        m_run = m_new;
-        // Anchored accumulator: o holds O * 2^(m - anchor), so the reference's per-tile
-        // rescale O *= alpha (:344) is folded into this tile's O scale factor
-        //   O_t = alpha_t O_{t-1} + sP sV T_t   <=>   o_t = o_{t-1} + sP sV 2^(m_t - anchor) T_t
-        // (mathematically identical; no per-tile pass over O and no branch in the hot loop).
-        const float scale = sp * svb[t] * e_anchor;
 #pragma unroll
         for (int m = 0; m < KS; ++m) {
             const int d = 32 * m + col;
             const int8_t* vr = L + KBYTES + gi * 64 * D + d * 64;
-            v16f acc = {};
+            v16f acc[QPW];
+#pragma unroll
+            for (int j = 0; j < QPW; ++j) acc[j] = v16f{};
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz<64>(d)));
-                if constexpr (ABL & 2) {
-                    asm volatile("" : "+v"(acc) : "v"(vop), "v"(pop[ks]));
-                } else {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], acc, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < QPW; ++j) {
+                    if constexpr (ABL & 2) {  // opaque result, no instruction
+                        asm volatile("" : "=v"(acc[j]) : "v"(vop), "v"(pop[j][ks]));
+                    } else {
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[j][ks], acc[j], 0, 0, 0);
+                    }
                 }
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o[m][r] = fmaf(acc[r], scale, o[m][r]);
+            for (int j = 0; j < QPW; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[j][m][r] = fmaf(acc[j][r], scale[j], o[j][m][r]);
         }
     };
 
@@ -359,58 +355,68 @@ __global__ __launch_bounds__(WAVES * 64, (ABL & 512) ? 2 : 4) void qmha_fa_int8_
     for (int st = 0; st < nst; ++st) {
         const int buf = (ABL & 64) ? 0 : (st & 1);
         if (!(ABL & 64) && st + 1 < nst) issue(buf ^ 1, st + 1);  // buf^1 was released by the previous barrier
-        if (active && !(ABL & 16)) {
+        if (any_active && !(ABL & 16)) {
             const int g0 = st * SG;
             const int ngr = min(SG, G - g0);  // wave-uniform
             const int8_t* L = lds[buf];
-            if ((ABL & 256) && ngr == SG) {
-#pragma unroll
-                for (int gi = 0; gi < SG; ++gi) {
-                    const v16i sc = qk(L, gi);
-                    tile(L, gi, g0 + gi, sc);
-                }
-            } else if (ngr == SG) {
+            if ((FL & FL_PREFETCH) && ngr == SG) {
                 // straight-line stage: Q@K^T of tile gi+1 is issued before tile gi's softmax
-                v16i s_cur = qk(L, 0);
+                v16i s_cur[QPW], s_nxt[QPW];
+                qk(L, 0, s_cur);
 #pragma unroll
                 for (int gi = 0; gi < SG; ++gi) {
-                    v16i s_nxt = {};
-                    if (gi + 1 < SG) s_nxt = qk(L, gi + 1);
-                    // pin the pipeline depth to one tile: without this fence the scheduler
-                    // hoists every Q@K^T of the stage and the live S tiles cost occupancy
+                    if (gi + 1 < SG) qk(L, gi + 1, s_nxt);
+                    // pin the pipeline depth to one tile (the scheduler would hoist every
+                    // Q@K^T of the stage and the live S tiles cost registers)
                     __builtin_amdgcn_sched_barrier(0);
                     QMHA_ISA_MARK();
                     tile(L, gi, g0 + gi, s_cur);
                     QMHA_ISA_MARK();
                     __builtin_amdgcn_sched_barrier(0);
-                    s_cur = s_nxt;
+#pragma unroll
+                    for (int j = 0; j < QPW; ++j) s_cur[j] = s_nxt[j];
+                }
+            } else if (ngr == SG) {
+#pragma unroll
+                for (int gi = 0; gi < SG; ++gi) {
+                    v16i s[QPW];
+                    qk(L, gi, s);
+                    QMHA_ISA_MARK();
+                    tile(L, gi, g0 + gi, s);
+                    QMHA_ISA_MARK();
                 }
             } else {
-                for (int gi = 0; gi < ngr; ++gi) tile(L, gi, g0 + gi, qk(L, gi));
+                for (int gi = 0; gi < ngr; ++gi) {
+                    v16i s[QPW];
+                    qk(L, gi, s);
+                    tile(L, gi, g0 + gi, s);
+                }
             }
             // re-anchor (rare, once per stage): keep 2^(m - anchor) far from fp32 overflow
-            if (__builtin_amdgcn_ballot_w64(m_run - anchor > 48.0f)) {
-                const float f = __builtin_amdgcn_exp2f(anchor - m_run);
 #pragma unroll
-                for (int m = 0; m < KS; ++m)
+            for (int j = 0; j < QPW; ++j) {
+                if (__builtin_amdgcn_ballot_w64(m_run[j] - anchor[j] > 48.0f)) {
+                    const float f = __builtin_amdgcn_exp2f(anchor[j] - m_run[j]);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) o[m][r] *= f;
-                if constexpr (ABL & 128) l_run *= f;
-                anchor = m_run;
+                    for (int m = 0; m < KS; ++m)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) o[j][m][r] *= f;
+                    l_run[j] *= f;
+                    anchor[j] = m_run[j];
+                }
             }
         }
         if constexpr (!(ABL & 64)) __syncthreads();  // vmcnt(0) + barrier: stage st+1 landed, stage st released
     }
 
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20 -----------------
-    if (active) {
-        const float unanchor = __builtin_amdgcn_exp2f(anchor - m_run);  // o * 2^(anchor - m) = O
-        if constexpr (ABL & 128) l_run *= unanchor;
-        const bool ok = l_run > 1e-20f;
 #pragma unroll
-        for (int m = 0; m < KS; ++m)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[m][r] *= unanchor;
+    for (int j = 0; j < QPW; ++j) {
+        const int qg = (qb * WAVES + wave) * QPW + j;
+        if (qg >= G) continue;  // wave-uniform
+        const float unanchor = __builtin_amdgcn_exp2f(anchor[j] - m_run[j]);  // 2^(anchor - m)
+        const float l = l_run[j] * unanchor;
+        const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
         for (int m = 0; m < KS; ++m)
@@ -418,9 +424,270 @@ __global__ __launch_bounds__(WAVES * 64, (ABL & 512) ? 2 : 4) void qmha_fa_int8_
             for (int g4 = 0; g4 < 4; ++g4) {
                 v4f w;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = ok ? o[m][4 * g4 + j] / l_run : 0.0f;
+                for (int jj = 0; jj < 4; ++jj) w[jj] = ok ? (o[j][m][4 * g4 + jj] * unanchor) / l : 0.0f;
                 *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
             }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Software-pipelined main kernel (one Q group per wave).
+//
+// Iteration t runs the softmax of tile t on the VALU while the matrix core executes
+// P@V of tile t-1 and Q@K^T of tile t+1 -- all three independent -- so each wave covers its
+// own MFMA time with its own VALU work instead of relying on co-resident waves.  The order
+// inside an iteration is pinned with sched_barrier fences (chunks of softmax VALU between
+// single MFMAs); every chained MFMA pair is split by VALU work.
+// K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
+// barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
+// ---------------------------------------------------------------------------------------
+template <int D, int WAVES, int FL>
+__global__ __launch_bounds__(WAVES * 64, 2) void qmha_fa_int8_pipe_kernel(
+    const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sQ, const float* __restrict__ sK, const float* __restrict__ sV,
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    static_assert(D == 64, "pipelined schedule is written for d = 64 (2 k-steps, 2 d-blocks)");
+    constexpr int SG = 2, RING = 3;
+    constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
+    constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
+    constexpr int SBYTES = KBYTES + VBYTES;
+    constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    constexpr bool MAGIC = FL & FL_MAGIC;
+    __shared__ __attribute__((aligned(16))) int8_t lds[RING][SBYTES];
+
+    QMHA_ENABLE_AGPR_MFMA();
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, col = lane & 31;
+    const int qg = qb * WAVES + wave;
+    const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
+
+    v4i qop[2];
+    float cq = 0.0f;
+    if (active) {
+        const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
+        qop[0] = *reinterpret_cast<const v4i*>(qp);
+        qop[1] = *reinterpret_cast<const v4i*>(qp + 32);
+        cq = sQ[(size_t)bh * G + qg] * c_log2;
+    } else {
+        qop[0] = qop[1] = v4i{0, 0, 0, 0};
+    }
+    const int8_t* kbase = Ki + (size_t)bh * N * D;
+    const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
+    const float* skb = sK + (size_t)bh * G;
+    const float* svb = sV + (size_t)bh * G;
+    const int nst = (G + SG - 1) / SG;
+
+    auto issue = [&](int st) {
+        const int ngr = min(SG, G - st * SG);
+        const int8_t* ksrc = kbase + (size_t)st * KBYTES;
+        const char* vsrc = vbase + (size_t)st * VBYTES;
+        int8_t* L = lds[st % RING];
+#pragma unroll
+        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
+                const int idx = inst * 64 + lane;
+                const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
+                __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * D + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
+                const int idx = inst * 64 + lane;
+                const int grp = idx / (4 * D), w = idx % (4 * D);
+                const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
+                __builtin_amdgcn_global_load_lds((gptr_t)(vsrc + grp * 64 * D + d * 64 + 16 * cv),
+                                                 (lptr_t)(L + KBYTES + inst * 1024), 16, 0, 0);
+            }
+        }
+    };
+    // operand reads of tile t from the ring
+    auto kop_of = [&](int t, int ks) {
+        const int8_t* L = lds[(t >> 1) % RING];
+        const int krow = (t & 1) * 32 + col;
+        return *reinterpret_cast<const v4i*>(L + krow * D + 16 * ((2 * ks + half) ^ chunk_swz<D>(krow)));
+    };
+    auto vop_of = [&](int t, int m, int ks) {
+        const int8_t* L = lds[(t >> 1) % RING];
+        const int d = 32 * m + col;
+        return *reinterpret_cast<const v8h*>(L + KBYTES + (t & 1) * 64 * D + d * 64 +
+                                             16 * ((2 * ks + half) ^ chunk_swz<64>(d)));
+    };
+
+    v16i magic_blk;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) magic_blk[r] = MAGIC ? 0x4B400000 : 0;
+    if constexpr (MAGIC) asm volatile("" : "+v"(magic_blk));
+
+    v16f o0 = {}, o1 = {};      // O^T, d-blocks 0 and 1 (anchored)
+    float m_run = 0.0f;          // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
+    float l_run = 0.0f;          // l * 2^(anchor - m)
+    float anchor = 0.0f;
+    v16i s_cur, s_nxt;           // S^T of tiles t and t+1
+    v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
+    float scale_cur = 0.0f, scale_prev = 0.0f;
+    v16f a0, a1;                 // P@V accumulators of the pending tile
+
+    issue(0);
+    if (nst > 1) issue(1);
+    __syncthreads();
+    s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 0), qop[0], magic_blk, 0, 0, 0);
+    s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 1), qop[1], s_cur, 0, 0, 0);
+
+#define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
+    // one pipeline iteration; HP / HN (compile time): a tile t-1 to finish / a tile t+1 to start
+    auto iter = [&](int t, auto HP, auto HN) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        if (t & 1) {  // uniform
+            __syncthreads();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            if ((t >> 1) + 2 < nst) issue((t >> 1) + 2);
+        }
+        // operand reads for this iteration's MFMAs
+        v8h v00, v01, v10, v11;
+        v4i k0, k1;
+        if constexpr (has_prev) {
+            v00 = vop_of(t - 1, 0, 0);
+            v10 = vop_of(t - 1, 1, 0);
+            v01 = vop_of(t - 1, 0, 1);
+            v11 = vop_of(t - 1, 1, 1);
+        }
+        if constexpr (has_next) {
+            k0 = kop_of(t + 1, 0);
+            k1 = kop_of(t + 1, 1);
+        }
+        QMHA_FENCE();
+        // ---- A: row max, running max, P-tile max (fa_tc_int8_b.cu:286-303, :359)
+        const float c = cq * skb[t];
+        const int mxi = half_swap_max_i(tree_max16_i(s_cur));
+        const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
+        const float m_new = fmaxf(m_run, mx * c);
+        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
+        QMHA_FENCE();
+        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v00, pp0, v16f{}, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- B: P scale, scores of rows 0..7
+        const float sp = fmaxf(div127_fast(pmax), 1e-8f);
+        const float invp = rcp_fast(sp);
+        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
+        float x[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+            x[r] = fmaf(sv, c, -m_new);
+        }
+        QMHA_FENCE();
+        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v10, pp0, v16f{}, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- C: scores of rows 8..15
+#pragma unroll
+        for (int r = 8; r < 16; ++r) {
+            const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+            x[r] = fmaf(sv, c, -m_new);
+        }
+        QMHA_FENCE();
+        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v01, pp1, a0, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- D: p = exp2, rows 0..7
+        float p[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        QMHA_FENCE();
+        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k0, qop[0], magic_blk, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- E: p = exp2, rows 8..15
+#pragma unroll
+        for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        QMHA_FENCE();
+        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v11, pp1, a1, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- F: Pi = rint(p/sP) as exact f16 integers
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float q0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+            const float q1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+            const v2h h2 = __builtin_convertvector((v2f{q0, q1}), v2h);
+            if (r < 4) {
+                pc0[2 * r] = h2[0];
+                pc0[2 * r + 1] = h2[1];
+            } else {
+                pc1[2 * r - 8] = h2[0];
+                pc1[2 * r - 7] = h2[1];
+            }
+        }
+        QMHA_FENCE();
+        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k1, qop[1], s_nxt, 0, 0, 0);
+        QMHA_FENCE();
+        // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
+        const float rs = half_swap_add(tree_sum16(p));
+        l_run = fmaf(rs, e, l_run);
+        m_run = m_new;
+        const float scale_t = sp * svb[t] * e;
+        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
+        if constexpr (has_prev) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o0[r] = fmaf(a0[r], scale_prev, o0[r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o1[r] = fmaf(a1[r], scale_prev, o1[r]);
+        }
+        QMHA_FENCE();
+        scale_cur = scale_t;
+        // re-anchor (rare): keep 2^(m - anchor) far from fp32 overflow; the tile whose P@V is
+        // still pending carries its factor in scale_cur
+        if (__builtin_amdgcn_ballot_w64(m_run - anchor > 48.0f)) {
+            const float f = __builtin_amdgcn_exp2f(anchor - m_run);
+            o0 *= f;
+            o1 *= f;
+            l_run *= f;
+            scale_cur *= f;
+            anchor = m_run;
+        }
+        // rotate the pipeline
+        pp0 = pc0;
+        pp1 = pc1;
+        scale_prev = scale_cur;
+        s_cur = s_nxt;
+    };
+    using T1 = std::integral_constant<bool, true>;
+    using F0 = std::integral_constant<bool, false>;
+    // G >= 2 (the launcher routes N < 64 elsewhere): first, interior, last tile
+    iter(0, F0{}, T1{});
+    for (int t = 1; t < G - 1; ++t) iter(t, T1{}, T1{});
+    iter(G - 1, T1{}, F0{});
+#undef QMHA_FENCE
+    // drain: P@V of the last tile
+    {
+        const int t = G - 1;
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 0, 0), pp0, v16f{}, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 1, 0), pp0, v16f{}, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 0, 1), pp1, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 1, 1), pp1, a1, 0, 0, 0);
+        o0 += a0 * scale_prev;
+        o1 += a1 * scale_prev;
+    }
+    // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
+    if (active) {
+        const float unanchor = __builtin_amdgcn_exp2f(anchor - m_run);
+        const float l = l_run * unanchor;
+        const bool ok = l > 1e-20f;
+        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            v4f w0, w1;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                w0[jj] = ok ? (o0[4 * g4 + jj] * unanchor) / l : 0.0f;
+                w1[jj] = ok ? (o1[4 * g4 + jj] * unanchor) / l : 0.0f;
+            }
+            *reinterpret_cast<v4f*>(orow + 8 * g4) = w0;
+            *reinterpret_cast<v4f*>(orow + 32 + 8 * g4) = w1;
+        }
     }
 }
 
@@ -489,53 +756,61 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
     }
 }
 
-template <int D, int WAVES, int SG, int ABL = 0>
+template <int D, int WAVES, int QPW, int SG, int FL, int ABL = 0>
 static hipError_t fa_int8_launch(const Int8Workspace& w, float* O, int B, int N, int H, int d_model,
                                  hipStream_t stream) {
     const int G = N / QMHA_GROUP;
-    const int nqb = (G + WAVES - 1) / WAVES;
+    const int nqb = (G + WAVES * QPW - 1) / (WAVES * QPW);
     const int nwg = B * H * nqb;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;  // inv_sqrt_d: fa_tc_int8_b.cu:587
-    hipLaunchKernelGGL((qmha_fa_int8_kernel<D, WAVES, SG, ABL>), dim3(nwg), dim3(WAVES * 64), 0, stream, w.Qi, w.Ki, w.Vh,
-                       w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+    hipLaunchKernelGGL((qmha_fa_int8_kernel<D, WAVES, QPW, SG, FL, ABL>), dim3(nwg), dim3(WAVES * 64), 0, stream, w.Qi,
+                       w.Ki, w.Vh, w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
 
+template <int D, int WAVES, int FL>
+static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, float* O, int B, int N, int H, int d_model,
+                                      hipStream_t stream) {
+    const int G = N / QMHA_GROUP;
+    if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);  // no pipeline to fill
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qi,
+                       w.Ki, w.Vh, w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+    return hipGetLastError();
+}
+
+// Default geometry per head size, and the QMHA_INT8_CFG tuning alternatives (profiling).
 template <int D>
 static hipError_t fa_int8_d(const Int8Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
     if constexpr (D == 64) {
-        switch (tune_config("QMHA_INT8_CFG")) {
-            case 44: return fa_int8_launch<D, 4, 4>(w, O, B, N, H, d_model, stream);
-            case 82: return fa_int8_launch<D, 8, 2>(w, O, B, N, H, d_model, stream);
-            default: break;
-        }
 #ifdef QMHA_ABLATION
         static const int abl = std::getenv("QMHA_INT8_ABL") ? std::atoi(std::getenv("QMHA_INT8_ABL")) : 0;
         switch (abl) {
-            case 1: return fa_int8_launch<D, 4, 2, 1>(w, O, B, N, H, d_model, stream);
-            case 2: return fa_int8_launch<D, 4, 2, 2>(w, O, B, N, H, d_model, stream);
-            case 4: return fa_int8_launch<D, 4, 2, 4>(w, O, B, N, H, d_model, stream);
-            case 6: return fa_int8_launch<D, 4, 2, 6>(w, O, B, N, H, d_model, stream);
-            case 8: return fa_int8_launch<D, 4, 2, 8>(w, O, B, N, H, d_model, stream);
-            case 9: return fa_int8_launch<D, 4, 2, 9>(w, O, B, N, H, d_model, stream);
-            case 15: return fa_int8_launch<D, 4, 2, 15>(w, O, B, N, H, d_model, stream);
-            case 16: return fa_int8_launch<D, 4, 2, 16>(w, O, B, N, H, d_model, stream);
-            case 32: return fa_int8_launch<D, 4, 2, 32>(w, O, B, N, H, d_model, stream);
-            case 64: return fa_int8_launch<D, 4, 2, 64>(w, O, B, N, H, d_model, stream);
-            case 128: return fa_int8_launch<D, 4, 2, 128>(w, O, B, N, H, d_model, stream);
-            case 384: return fa_int8_launch<D, 4, 2, 384>(w, O, B, N, H, d_model, stream);
-            case 256: return fa_int8_launch<D, 4, 2, 256>(w, O, B, N, H, d_model, stream);
-            case 512: return fa_int8_launch<D, 4, 2, 512>(w, O, B, N, H, d_model, stream);
-            case 640: return fa_int8_launch<D, 4, 2, 640>(w, O, B, N, H, d_model, stream);
-            case 896: return fa_int8_launch<D, 4, 2, 896>(w, O, B, N, H, d_model, stream);
-            case 65: return fa_int8_launch<D, 4, 2, 65>(w, O, B, N, H, d_model, stream);
-            case 70: return fa_int8_launch<D, 4, 2, 70>(w, O, B, N, H, d_model, stream);
-            case 79: return fa_int8_launch<D, 4, 2, 79>(w, O, B, N, H, d_model, stream);
+            case 1: return fa_int8_launch<D, 4, 1, 2, 0, 1>(w, O, B, N, H, d_model, stream);
+            case 2: return fa_int8_launch<D, 4, 1, 2, 0, 2>(w, O, B, N, H, d_model, stream);
+            case 4: return fa_int8_launch<D, 4, 1, 2, 0, 4>(w, O, B, N, H, d_model, stream);
+            case 16: return fa_int8_launch<D, 4, 1, 2, 0, 16>(w, O, B, N, H, d_model, stream);
+            case 64: return fa_int8_launch<D, 4, 1, 2, 0, 64>(w, O, B, N, H, d_model, stream);
+            case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, O, B, N, H, d_model, stream);
+            case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, O, B, N, H, d_model, stream);
+            case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
+        switch (tune_config("QMHA_INT8_CFG")) {
+            case 4120: return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);
+            case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, O, B, N, H, d_model, stream);
+            case 4125: return fa_int8_launch<D, 4, 1, 2, FL_MAGIC | FL_LB2>(w, O, B, N, H, d_model, stream);
+            case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, O, B, N, H, d_model, stream);
+            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, O, B, N, H, d_model, stream);
+            case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, O, B, N, H, d_model, stream);
+            default: break;
+        }
+        // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
+        return fa_int8_pipe_launch<D, 4, 0>(w, O, B, N, H, d_model, stream);
     }
-    return fa_int8_launch<D, 4, 2>(w, O, B, N, H, d_model, stream);
+    return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, float* O, int B, int N, int H, int D, int d_model,

@@ -35,6 +35,8 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                 "-mllvm", "-amdgpu-mfma-vgpr-form"]
 # profiling builds only, e.g. QMHA_EXTRA_FLAGS=-DQMHA_ABLATION (rebuild with --clean)
 COMMON_FLAGS += os.environ.get("QMHA_EXTRA_FLAGS", "").split()
+if os.environ.get("QMHA_AGPR_FORM"):  # A/B: let MFMA accumulators live in AGPRs
+    COMMON_FLAGS = [f for f in COMMON_FLAGS if f not in ("-mllvm", "-amdgpu-mfma-vgpr-form")] + ["-DQMHA_MFMA_AGPR"]
 
 
 def newer(target, deps):
