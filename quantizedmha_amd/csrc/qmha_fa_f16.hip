@@ -269,6 +269,198 @@ __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Main kernel v2: K/V staged by LDS-DMA (global_load_lds, swizzled source / linear LDS image),
+// one 32-key tile at a time, Q@K^T of the next tile issued before the current softmax
+// (FL_PREFETCH).  One wave = one 32-row Q group.
+// ---------------------------------------------------------------------------------------
+enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4 };
+
+template <int D, int WAVES, int SG, int FL>
+__global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f16_v2_kernel(
+    const _Float16* __restrict__ Qh, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    QMHA_ENABLE_AGPR_MFMA();
+    constexpr int KS = D / 16;           // QK k-steps (K = 16)
+    constexpr int MB = D / 32;           // PV d-blocks
+    constexpr int RB = 2 * D;            // K row bytes
+    constexpr int KBYTES = SG * 32 * RB; // K per stage
+    constexpr int VBYTES = SG * 32 * D * 2;
+    constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    static_assert(KCH % 64 == 0 && VCH % 64 == 0 && (KCH / SG) % 64 == 0, "whole KiB LDS-DMA pieces");
+    __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
+
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int qg = qb * WAVES + wave;
+    const bool active = qg < G;
+    const int half = lane >> 5, col = lane & 31;
+
+    v8h qop[KS];
+    if (active) {
+        const _Float16* qp = Qh + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 8 * half;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) qop[s] = *reinterpret_cast<const v8h*>(qp + 16 * s);
+    } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qop[s][e] = (_Float16)0.0f;
+    }
+    v16f o[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) o[m] = v16f{};
+    float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290)
+    unsigned long long stamp[4] = {0, 0, 0, 0};  // F16_STAMP diagnostics only
+    const unsigned long long k_t0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long k_r0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    const char* kbase = reinterpret_cast<const char*>(Kh + (size_t)bh * N * D);
+    const char* vbase = reinterpret_cast<const char*>(Vt + (size_t)bh * N * D);
+    const int nst = (G + SG - 1) / SG;
+
+    auto issue = [&](int buf, int st) {
+        const int ngr = min(SG, G - st * SG);
+        const char* ksrc = kbase + (size_t)st * KBYTES;
+        const char* vsrc = vbase + (size_t)st * VBYTES;
+        char* L = lds[buf];
+#pragma unroll
+        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
+                const int idx = inst * 64 + lane;
+                const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ chunk_swz_h<RB>(row);
+                __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * RB + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
+                const int idx = inst * 64 + lane;
+                const int grp = idx / (4 * D), w = idx % (4 * D);
+                const int d = w >> 2, cv = (w & 3) ^ chunk_swz_h<64>(d);
+                __builtin_amdgcn_global_load_lds((gptr_t)(vsrc + grp * 64 * D + d * 64 + 16 * cv),
+                                                 (lptr_t)(L + KBYTES + inst * 1024), 16, 0, 0);
+            }
+        }
+    };
+    // S^T = K Q^T (fp32 accumulate) of tile gi of the stage in LDS
+    auto qk = [&](const char* L, int gi) {
+        v16f s = {};
+        const int krow = gi * 32 + col;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
+            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
+        }
+        return s;
+    };
+    // online softmax of one tile (fa_tc_v1a.cu:101-220) and O = alpha*O + P V (:207,:218)
+    auto tile = [&](const char* L, int gi, const v16f& s) {
+        float mx = s[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
+        mx = half_swap_max(mx);
+        const float m_new = fmaxf(m_run, mx * c_log2);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        float p[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_new));
+        v8h pop[2];
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const v2h h2 = __builtin_convertvector((v2f{p[r], p[r + 1]}), v2h);  // __float2half (RNE), :174
+            pop[r >> 3][r & 7] = h2[0];
+            pop[r >> 3][(r & 7) + 1] = h2[1];
+        }
+        const float rs = half_swap_add(tree_sum16(p));
+        l_run = fmaf(alpha, l_run, rs);  // :198
+        m_run = m_new;
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {  // exact skip when alpha == 1 for every row
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= alpha;
+        }
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            const int d = 32 * m + col;
+            const char* vr = L + KBYTES + gi * 64 * D + d * 64;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
+            }
+        }
+    };
+
+    issue(0, 0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) issue(buf ^ 1, st + 1);
+        if (active) {
+            const int ngr = min(SG, G - st * SG);
+            const char* L = lds[buf];
+            if ((FL & F16_PREFETCH) && ngr == SG) {
+                v16f s_cur = qk(L, 0);
+#pragma unroll
+                for (int gi = 0; gi < SG; ++gi) {
+                    v16f s_nxt = {};
+                    if (gi + 1 < SG) s_nxt = qk(L, gi + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    tile(L, gi, s_cur);
+                    __builtin_amdgcn_sched_barrier(0);
+                    s_cur = s_nxt;
+                }
+            } else if constexpr (FL & F16_STAMP) {
+                for (int gi = 0; gi < ngr; ++gi) {
+                    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                    v16f s = qk(L, gi);
+                    asm volatile("" : "+v"(s));
+                    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+                    const float x = s[0] + s[7] + s[15];  // forces the QK result
+                    asm volatile("" :: "v"(x));
+                    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+                    tile(L, gi, s);
+                    asm volatile("" : "+v"(o[0]));
+                    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                    stamp[0] += t1 - t0;
+                    stamp[1] += t2 - t1;
+                    stamp[2] += t3 - t2;
+                }
+            } else {
+                for (int gi = 0; gi < ngr; ++gi) tile(L, gi, qk(L, gi));
+            }
+        }
+        const unsigned long long tb = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
+        __syncthreads();
+        if constexpr (FL & F16_STAMP) stamp[3] += __builtin_amdgcn_s_memtime() - tb;
+    }
+    if constexpr (FL & F16_STAMP) {
+        if (lane == 0 && (blockIdx.x % 997) == 0)
+            printf("stamp wg %d wave %d: qk_issue %llu qk_wait %llu tile %llu barrier %llu (tiles %d) total %llu real100MHz %llu\n",
+                   (int)blockIdx.x, wave, stamp[0], stamp[1], stamp[2], stamp[3], G,
+                   __builtin_amdgcn_s_memtime() - k_t0, __builtin_amdgcn_s_memrealtime() - k_r0);
+    }
+    if (active) {
+        const bool ok = l_run > 1e-10f;  // fa_tc_v1a.cu:384-388
+        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                v4f w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = ok ? o[m][4 * g4 + j] / l_run : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
+            }
+    }
+}
+
 size_t f16_workspace_bytes(int B, int N, int H, int D) {
     return 3 * align_up((size_t)B * H * N * D * 2, 256);
 }
@@ -313,16 +505,39 @@ static hipError_t fa_f16_launch(const F16Workspace& w, float* O, int B, int N, i
     return hipGetLastError();
 }
 
+template <int D, int WAVES, int SG, int FL>
+static hipError_t fa_f16_v2_launch(const F16Workspace& w, float* O, int B, int N, int H, int d_model,
+                                   hipStream_t stream) {
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;
+    hipLaunchKernelGGL((qmha_fa_f16_v2_kernel<D, WAVES, SG, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qh,
+                       w.Kh, w.Vt, O, N, H, d_model, nqb, c_log2);
+    return hipGetLastError();
+}
+
 template <int D>
 static hipError_t fa_f16_d(const F16Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
     if constexpr (D == 64) {
         switch (tune_config("QMHA_F16_CFG")) {
             case 82: return fa_f16_launch<D, 8, 2>(w, O, B, N, H, d_model, stream);
             case 22: return fa_f16_launch<D, 2, 2>(w, O, B, N, H, d_model, stream);
+            case 420: return fa_f16_v2_launch<D, 4, 2, 0>(w, O, B, N, H, d_model, stream);
+            case 421: return fa_f16_v2_launch<D, 4, 2, F16_PREFETCH>(w, O, B, N, H, d_model, stream);
+            case 440: return fa_f16_v2_launch<D, 4, 4, 0>(w, O, B, N, H, d_model, stream);
+            case 441: return fa_f16_v2_launch<D, 4, 4, F16_PREFETCH>(w, O, B, N, H, d_model, stream);
+            case 424: return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, O, B, N, H, d_model, stream);
+            case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, O, B, N, H, d_model, stream);
+#ifdef QMHA_ABLATION
+            case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, O, B, N, H, d_model, stream);
+            case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, O, B, N, H, d_model, stream);
+#endif
             default: break;
         }
     }
-    return fa_f16_launch<D, 4, 2>(w, O, B, N, H, d_model, stream);
+    // default: v2 (LDS-DMA staging, per-tile softmax), 4 waves/SIMD budget (r01 A/B: 1.54 ms vs
+    // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64)
+    return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,
