@@ -107,11 +107,16 @@ const char *qmha_last_error(void);
 
 /*
  * Kernel timing for roofline reporting (bench.py): when enabled, qmha_solve_* record a
- * hipEvent pair around the dominant ("main") kernel of every call.  qmha_profile_collect
- * synchronises those events and returns the summed main-kernel milliseconds and the
- * launch count since the last collect, then clears the record.
+ * hipEvent pair around every launch of the dominant ("main") kernel and of the pre-pass.
+ * The int8 and fp16 paths split a call into batch chunks whose pre-pass runs on a library
+ * stream, overlapped with the previous chunk's main kernel (QMHA_OVERLAP_CHUNKS, default 1 = off).
+ * qmha_profile_collect synchronises those events and returns the summed main-kernel and
+ * pre-pass milliseconds and the number of calls since the last collect, then clears the record.
  */
 void qmha_profile_enable(int on);
+/* Number of batch chunks for the pre-pass / main-kernel overlap (1..16, 1 = off); returns the
+ * previous value.  Results are bit-identical for every setting. */
+int qmha_set_overlap_chunks(int n);
 int qmha_profile_collect(double *main_ms, long long *launches, double *prepass_ms);
 
 /* Release all library-owned workspaces (optional; also released at process exit). */

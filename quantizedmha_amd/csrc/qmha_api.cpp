@@ -5,6 +5,7 @@
 // heads in one grid, and errors are reported instead of ignored.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -70,9 +71,10 @@ int check_shape(const void* Q, const void* K, const void* V, const void* O, int 
 }
 
 // ---- profiling --------------------------------------------------------------------------
+// Per call: event pairs around every pre-pass launch (on the pre-pass stream) and every main
+// launch (on the caller's stream); qmha_profile_collect sums them per call.
 struct ProfRec {
-    hipEvent_t e0, e1, e2;  // e0 -> e1 pre-pass, e1 -> e2 main kernel
-    bool has_pre;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pre, main;
 };
 std::mutex g_prof_mu;
 bool g_prof_on = false;
@@ -88,6 +90,52 @@ hipEvent_t take_event() {
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
+}
+
+// ---- pre-pass / main-kernel overlap (int8 and fp16 paths) ------------------------------
+// The HBM-bound pre-pass (quantise / convert) of batch chunk c+1 runs on a library-owned
+// second stream while the compute-bound main kernel of chunk c runs on the caller's stream.
+// Chunks are disjoint slices of the same workspace arrays, so only "pre(c) before main(c)"
+// and "previous call done before pre(0)" need ordering.  QMHA_OVERLAP_CHUNKS (default 1 =
+// off: measured slower at C4, the co-running pre-pass slows the main kernel more than it hides,
+// profiles/r01/overlap_sweep.txt) sets the number of chunks.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t start = nullptr;
+    std::vector<hipEvent_t> ready;
+};
+std::mutex g_side_mu;
+std::map<std::pair<int, void*>, SideStream> g_side;
+
+std::atomic<int> g_overlap_chunks{-1};  // -1: not yet read from QMHA_OVERLAP_CHUNKS
+
+int overlap_chunks(int B) {
+    int c = g_overlap_chunks.load();
+    if (c < 0) {
+        const char* e = std::getenv("QMHA_OVERLAP_CHUNKS");
+        c = e ? std::atoi(e) : 1;
+        c = c < 1 ? 1 : (c > 16 ? 16 : c);
+        g_overlap_chunks.store(c);
+    }
+    return c > B ? B : c;
+}
+
+int get_side(hipStream_t stream, int nchunks, SideStream** out) {
+    int dev = 0;
+    QMHA_HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    SideStream& ss = g_side[{dev, (void*)stream}];
+    if (!ss.s) {
+        QMHA_HIP_TRY(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking), "hipStreamCreate");
+        QMHA_HIP_TRY(hipEventCreateWithFlags(&ss.start, hipEventDisableTiming), "hipEventCreate");
+    }
+    while ((int)ss.ready.size() < nchunks) {
+        hipEvent_t e = nullptr;
+        QMHA_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        ss.ready.push_back(e);
+    }
+    *out = &ss;
+    return QMHA_OK;
 }
 
 // ---- library-owned workspaces, one per (device, stream) --------------------------------
@@ -139,6 +187,15 @@ size_t workspace_bytes(int B, int N, int H, int D, int variant) {
     }
 }
 
+qmha::Int8Workspace int8_slice(const qmha::Int8Workspace& w, size_t b0, int N, int H, int D) {
+    const size_t e = b0 * H * N * D, g = b0 * H * (N / 32);  // 32-row quantisation groups
+    return qmha::Int8Workspace{w.Qi + e, w.Ki + e, w.Vh + e, w.sQ + g, w.sK + g, w.sV + g};
+}
+qmha::F16Workspace f16_slice(const qmha::F16Workspace& w, size_t b0, int N, int H, int D) {
+    const size_t e = b0 * H * N * D;
+    return qmha::F16Workspace{w.Qh + e, w.Kh + e, w.Vt + e};
+}
+
 int run(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model, int h, int variant,
         void* ws, size_t ws_bytes, hipStream_t stream) {
     const int D = d_model / h;
@@ -147,54 +204,91 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
         g_last_error = "workspace too small";
         return QMHA_ERR_INVALID;
     }
-    ProfRec rec{nullptr, nullptr, nullptr, false};
     bool prof;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         prof = g_prof_on;
-        if (prof) {
-            rec.e0 = take_event();
-            rec.e1 = take_event();
-            rec.e2 = take_event();
-            if (!rec.e0 || !rec.e1 || !rec.e2) prof = false;
-        }
     }
-    if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e0, stream), "hipEventRecord");
-    switch (variant) {
-        case QMHA_FA_TC_INT8_B: {
-            qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
-            QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, 1, B, N, h, D, d_model, stream), "quant_int8 launch");
-            rec.has_pre = true;
-            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
-            QMHA_HIP_TRY(qmha::launch_fa_int8_main(w, O, B, N, h, D, d_model, stream), "fa_int8 launch");
-            break;
+    ProfRec rec;
+    auto mark = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t s, bool begin) -> int {
+        if (!prof) return QMHA_OK;
+        hipEvent_t e;
+        {
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            e = take_event();
         }
-        case QMHA_FA_TC_V1A: {
-            qmha::F16Workspace w = qmha::f16_carve(ws, B, N, h, D);
-            QMHA_HIP_TRY(qmha::launch_convert_f16(Q, K, V, w, B, N, h, D, d_model, stream), "convert_f16 launch");
-            rec.has_pre = true;
-            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
-            QMHA_HIP_TRY(qmha::launch_fa_f16_main(w, O, B, N, h, D, d_model, stream), "fa_f16 launch");
-            break;
+        if (!e) {
+            g_last_error = "hipEventCreate failed";
+            return QMHA_ERR_HIP;
         }
-        case QMHA_FA: {
-            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
-            QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, stream), "fa_f32 launch");
-            break;
+        if (begin) v.push_back({e, nullptr});
+        else v.back().second = e;
+        QMHA_HIP_TRY(hipEventRecord(e, s), "hipEventRecord");
+        return QMHA_OK;
+    };
+#define QMHA_MARK(vec, s, begin)                       \
+    do {                                               \
+        int _st = mark(vec, s, begin);                 \
+        if (_st != QMHA_OK) return _st;                \
+    } while (0)
+
+    if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
+        const size_t slab = (size_t)N * d_model;  // floats per sequence
+        const int nc = overlap_chunks(B);
+        SideStream* side = nullptr;
+        if (nc > 1) {
+            int st = get_side(stream, nc, &side);
+            if (st != QMHA_OK) return st;
+            QMHA_HIP_TRY(hipEventRecord(side->start, stream), "hipEventRecord");
+            QMHA_HIP_TRY(hipStreamWaitEvent(side->s, side->start, 0), "hipStreamWaitEvent");
         }
-        case QMHA_UNFUSED: {
-            if (prof) QMHA_HIP_TRY(hipEventRecord(rec.e1, stream), "hipEventRecord");
-            QMHA_HIP_TRY(qmha::launch_unfused(Q, K, V, O, ws, B, N, h, D, d_model, stream), "unfused launch");
-            break;
+        const hipStream_t pre_s = nc > 1 ? side->s : stream;
+        const qmha::Int8Workspace w8 = variant == QMHA_FA_TC_INT8_B ? qmha::int8_carve(ws, B, N, h, D) : qmha::Int8Workspace{};
+        const qmha::F16Workspace w16 = variant == QMHA_FA_TC_V1A ? qmha::f16_carve(ws, B, N, h, D) : qmha::F16Workspace{};
+        // every pre-pass is enqueued first (the side stream runs ahead), then the main kernels
+        for (int c = 0; c < nc; ++c) {
+            const int b0 = (int)((long long)B * c / nc), b1 = (int)((long long)B * (c + 1) / nc), nb = b1 - b0;
+            QMHA_MARK(rec.pre, pre_s, true);
+            if (variant == QMHA_FA_TC_INT8_B) {
+                const qmha::Int8Workspace w = int8_slice(w8, b0, N, h, D);
+                QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, 1, nb, N, h, D,
+                                                     d_model, pre_s), "quant_int8 launch");
+            } else {
+                QMHA_HIP_TRY(qmha::launch_convert_f16(Q + b0 * slab, K + b0 * slab, V + b0 * slab, f16_slice(w16, b0, N, h, D),
+                                                      nb, N, h, D, d_model, pre_s), "convert_f16 launch");
+            }
+            QMHA_MARK(rec.pre, pre_s, false);
+            if (nc > 1) QMHA_HIP_TRY(hipEventRecord(side->ready[c], pre_s), "hipEventRecord");
         }
-        default:
-            g_last_error = "unknown variant";
-            return QMHA_ERR_INVALID;
+        for (int c = 0; c < nc; ++c) {
+            const int b0 = (int)((long long)B * c / nc), b1 = (int)((long long)B * (c + 1) / nc), nb = b1 - b0;
+            if (nc > 1) QMHA_HIP_TRY(hipStreamWaitEvent(stream, side->ready[c], 0), "hipStreamWaitEvent");
+            QMHA_MARK(rec.main, stream, true);
+            if (variant == QMHA_FA_TC_INT8_B) {
+                QMHA_HIP_TRY(qmha::launch_fa_int8_main(int8_slice(w8, b0, N, h, D), O + b0 * slab, nb, N, h, D, d_model, stream),
+                             "fa_int8 launch");
+            } else {
+                QMHA_HIP_TRY(qmha::launch_fa_f16_main(f16_slice(w16, b0, N, h, D), O + b0 * slab, nb, N, h, D, d_model, stream),
+                             "fa_f16 launch");
+            }
+            QMHA_MARK(rec.main, stream, false);
+        }
+    } else if (variant == QMHA_FA) {
+        QMHA_MARK(rec.main, stream, true);
+        QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, stream), "fa_f32 launch");
+        QMHA_MARK(rec.main, stream, false);
+    } else if (variant == QMHA_UNFUSED) {
+        QMHA_MARK(rec.main, stream, true);
+        QMHA_HIP_TRY(qmha::launch_unfused(Q, K, V, O, ws, B, N, h, D, d_model, stream), "unfused launch");
+        QMHA_MARK(rec.main, stream, false);
+    } else {
+        g_last_error = "unknown variant";
+        return QMHA_ERR_INVALID;
     }
+#undef QMHA_MARK
     if (prof) {
-        QMHA_HIP_TRY(hipEventRecord(rec.e2, stream), "hipEventRecord");
         std::lock_guard<std::mutex> lk(g_prof_mu);
-        g_prof_recs.push_back(rec);
+        g_prof_recs.push_back(std::move(rec));
     }
     return QMHA_OK;
 }
@@ -339,6 +433,12 @@ const char* qmha_version(void) { return QMHA_VERSION_STRING; }
 
 const char* qmha_last_error(void) { return g_last_error.c_str(); }
 
+int qmha_set_overlap_chunks(int n) {
+    const int prev = overlap_chunks(1 << 30);
+    g_overlap_chunks.store(n < 1 ? 1 : (n > 16 ? 16 : n));
+    return prev;
+}
+
 void qmha_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;
@@ -352,22 +452,23 @@ int qmha_profile_collect(double* main_ms, long long* launches, double* prepass_m
     }
     double tm = 0.0, tp = 0.0;
     for (auto& r : recs) {
-        QMHA_HIP_TRY(hipEventSynchronize(r.e2), "hipEventSynchronize");
-        float a = 0.0f, b = 0.0f;
-        QMHA_HIP_TRY(hipEventElapsedTime(&a, r.e1, r.e2), "hipEventElapsedTime");
-        tm += a;
-        if (r.has_pre) {
-            QMHA_HIP_TRY(hipEventElapsedTime(&b, r.e0, r.e1), "hipEventElapsedTime");
-            tp += b;
+        for (auto* v : {&r.main, &r.pre}) {
+            for (auto& pr : *v) {
+                QMHA_HIP_TRY(hipEventSynchronize(pr.second), "hipEventSynchronize");
+                float a = 0.0f;
+                QMHA_HIP_TRY(hipEventElapsedTime(&a, pr.first, pr.second), "hipEventElapsedTime");
+                (v == &r.main ? tm : tp) += a;
+            }
         }
     }
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
-        for (auto& r : recs) {
-            g_event_pool.push_back(r.e0);
-            g_event_pool.push_back(r.e1);
-            g_event_pool.push_back(r.e2);
-        }
+        for (auto& r : recs)
+            for (auto* v : {&r.main, &r.pre})
+                for (auto& pr : *v) {
+                    g_event_pool.push_back(pr.first);
+                    g_event_pool.push_back(pr.second);
+                }
     }
     if (main_ms) *main_ms = tm;
     if (prepass_ms) *prepass_ms = tp;
@@ -376,6 +477,16 @@ int qmha_profile_collect(double* main_ms, long long* launches, double* prepass_m
 }
 
 void qmha_release_workspaces(void) {
+    {
+        std::lock_guard<std::mutex> lk(g_side_mu);
+        for (auto& kv : g_side) {
+            (void)hipStreamSynchronize(kv.second.s);
+            for (hipEvent_t e : kv.second.ready) (void)hipEventDestroy(e);
+            (void)hipEventDestroy(kv.second.start);
+            (void)hipStreamDestroy(kv.second.s);
+        }
+        g_side.clear();
+    }
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (auto& kv : g_ws) {
         if (kv.second.ptr) {

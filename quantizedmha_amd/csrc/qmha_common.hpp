@@ -169,6 +169,15 @@ __device__ __forceinline__ uint32_t pack4_lowbytes(float a, float b, float c, fl
     return __builtin_amdgcn_perm(t23, t01, 0x05040100u);
 }
 
+// Workgroup barrier after LDS-DMA (global_load_lds): every wave first drains its own DMA
+// (vmcnt(0)) so that after the barrier all waves see the whole stage in LDS.  __syncthreads()
+// alone is not enough: the compiler may drop the vmcnt wait before s_barrier when no LDS read
+// of the issuing wave depends on it (observed in the pipelined int8 kernel -> a cross-wave race).
+__device__ __forceinline__ void qmha_dma_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 // XCD-aware remap of a linear workgroup id: the dispatcher deals ids round-robin over the
 // 8 XCDs, so give each XCD a contiguous range of work items (consecutive q-blocks of the
 // same head share K/V in that XCD's L2).  Bijective for any nwg (cdna guide T1).

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
                 for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (_Float16)v[i][c];
             }
         }
-        __syncthreads();
+        qmha_dma_barrier();
         if (active) {
             _Float16* dst = Vt + ((size_t)bh * G + g) * (size_t)(32 * D);
             constexpr int CH = 32 * D * 2 / 16;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
 
     gload(0);
     lstore(0, 0);
-    __syncthreads();
+    qmha_dma_barrier();
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) gload(st + 1);
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
             }
         }
         if (st + 1 < nst) lstore(buf ^ 1, st + 1);
-        __syncthreads();
+        qmha_dma_barrier();
     }
     if (active) {
         const bool ok = l_run > 1e-10f;
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     };
 
     issue(0, 0);
-    __syncthreads();
+    qmha_dma_barrier();
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) issue(buf ^ 1, st + 1);
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
             }
         }
         const unsigned long long tb = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
-        __syncthreads();
+        qmha_dma_barrier();
         if constexpr (FL & F16_STAMP) stamp[3] += __builtin_amdgcn_s_memtime() - tb;
     }
     if constexpr (FL & F16_STAMP) {

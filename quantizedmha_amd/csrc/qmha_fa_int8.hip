@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
                 for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (int8_t)qmha_quant_i8(v[i][c], inv);
             }
         }
-        __syncthreads();
+        qmha_dma_barrier();
         if (active) {
             int8_t* dst = static_cast<int8_t*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
             constexpr int CH = 32 * D / 16;
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
                 for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (_Float16)qmha_quant_i8(v[i][c], inv);
             }
         }
-        __syncthreads();
+        qmha_dma_barrier();
         if (active) {
             _Float16* dst = static_cast<_Float16*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
             constexpr int CH = 32 * D * 2 / 16;
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
     };
 
     issue(0, 0);
-    __syncthreads();  // waits vmcnt(0): stage 0 has landed
+    qmha_dma_barrier();  // waits vmcnt(0): stage 0 has landed
 
     for (int st = 0; st < nst; ++st) {
         const int buf = (ABL & 64) ? 0 : (st & 1);
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
                 }
             }
         }
-        if constexpr (!(ABL & 64)) __syncthreads();  // vmcnt(0) + barrier: stage st+1 landed, stage st released
+        if constexpr (!(ABL & 64)) qmha_dma_barrier();  // vmcnt(0) + barrier: stage st+1 landed, stage st released
     }
 
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20 -----------------
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void qmha_fa_int8_pipe_kernel(
 
     issue(0);
     if (nst > 1) issue(1);
-    __syncthreads();
+    qmha_dma_barrier();
     s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 0), qop[0], magic_blk, 0, 0, 0);
     s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 1), qop[1], s_cur, 0, 0, 0);
 
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void qmha_fa_int8_pipe_kernel(
     auto iter = [&](int t, auto HP, auto HN) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
         if (t & 1) {  // uniform
-            __syncthreads();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
             if ((t >> 1) + 2 < nst) issue((t >> 1) + 2);
         }
         // operand reads for this iteration's MFMAs

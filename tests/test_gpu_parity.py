@@ -228,3 +228,24 @@ def test_driver_binary_end_to_end(dev, tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         assert "Correctness check PASSED" in r.stdout
         assert '"check_random": "passed"' in r.stdout
+
+
+@pytest.mark.parametrize("variant", ["fa_tc_int8_b", "fa_tc_v1a"])
+def test_overlap_chunks_bit_identical(dev, variant):
+    """Batch-chunked pre-pass/main overlap (qmha_set_overlap_chunks) must not change a bit, and
+    two calls in a row on the same workspace must agree (catches LDS-DMA / stream races)."""
+    from quantizedmha_amd import _lib, torch_ext
+    lib = _lib.load()
+    B, N, H, d = 8, 1024, 16, 64
+    g = torch.Generator(device=dev).manual_seed(3)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    prev = lib.qmha_set_overlap_chunks(1)
+    try:
+        ref = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
+        for chunks in (2, 4):
+            lib.qmha_set_overlap_chunks(chunks)
+            for _ in range(2):
+                out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
+                assert torch.equal(out, ref), (variant, chunks)
+    finally:
+        lib.qmha_set_overlap_chunks(prev)

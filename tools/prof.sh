@@ -12,7 +12,9 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json | head -c 1500; echo
 if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1
+# the same bench command under the profiler (its JSON line lands in trace.log: its hipEvent
+# main_kernel_ms and rocprof's average for the main kernel describe the same launches)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1
 rc=$?; echo "rocprof trace rc=$rc"
 if [ $rc -ne 0 ]; then tail -20 $OUT/trace.log; exit $rc; fi
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
