@@ -24,7 +24,6 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
     _Float16* __restrict__ Qh, _Float16* __restrict__ Kh, _Float16* __restrict__ Vt,
     int N, int H, int d_model, int total_groups) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
-    __shared__ __attribute__((aligned(16))) _Float16 vtile[4][32 * D];
     const int tensor = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int item = blockIdx.x * 4 + wave;
@@ -33,6 +32,24 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
     const int bh = active ? item / G : 0, g = active ? item % G : 0;
     const int b = bh / H, k = bh % H;
     const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
+    if (tensor == 2) {
+        // V^T operand order without an LDS transpose (see qmha_quant_int8_kernel): lane unit
+        // u = lane + 64 i writes the 8-slot chunk j = u / D of row d = u % D
+        if (active) {
+            constexpr int UPL = D / 16;
+            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D;
+            _Float16* dst = Vt + ((size_t)bh * G + g) * (size_t)(32 * D);
+#pragma unroll
+            for (int i = 0; i < UPL; ++i) {
+                const int u = lane + 64 * i, d = u % D, j = u / D;
+                v8h h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (_Float16)base[(size_t)kv_of_slot_f16(8 * j + e) * d_model + d];
+                *reinterpret_cast<v8h*>(dst + d * 32 + 8 * j) = h;
+            }
+        }
+        return;
+    }
     const int ri = lane / C4, ci = lane % C4;
     v4f v[NI];
     if (active) {
@@ -40,35 +57,15 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
 #pragma unroll
         for (int i = 0; i < NI; ++i) v[i] = *reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model);
     }
-    if (tensor < 2) {
-        if (active) {
-            _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+    if (active) {  // Q, K: f16 rows
+        _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                typedef _Float16 v4h __attribute__((ext_vector_type(4)));
-                v4h hv;
+        for (int i = 0; i < NI; ++i) {
+            typedef _Float16 v4h __attribute__((ext_vector_type(4)));
+            v4h hv;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)
-                *reinterpret_cast<v4h*>(dst + (size_t)(i * RPI + ri) * D) = hv;
-            }
-        }
-    } else {
-        _Float16* tile = vtile[wave];
-        if (active) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int slot = slot_of_kv_f16(i * RPI + ri);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (_Float16)v[i][c];
-            }
-        }
-        qmha_dma_barrier();
-        if (active) {
-            _Float16* dst = Vt + ((size_t)bh * G + g) * (size_t)(32 * D);
-            constexpr int CH = 32 * D * 2 / 16;
-#pragma unroll
-            for (int c = lane; c < CH; c += 64)
-                reinterpret_cast<v4i*>(dst)[c] = reinterpret_cast<const v4i*>(tile)[c];
+            for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)
+            *reinterpret_cast<v4h*>(dst + (size_t)(i * RPI + ri) * D) = hv;
         }
     }
 }

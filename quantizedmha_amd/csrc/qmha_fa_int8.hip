@@ -64,6 +64,44 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const int b = bh / H, k = bh % H;
     const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
 
+    if (tensor == 2 && v_mode == 1) {
+        // V straight into the f16 V^T operand order without an LDS transpose: lane unit
+        // u = lane + 64 i owns output chunk (d = u % D, slot chunk j = u / D), i.e. 8 values
+        // V[kv_of_slot_f16(8j + e)][d]; for a fixed (i, e) the lanes read consecutive d of one
+        // row (coalesced).  (The former LDS transpose ran into 16-way bank conflicts.)
+        constexpr int UPL = D / 16;  // units per lane
+        float x[UPL][8];
+        float amax = 0.0f;
+        if (active) {
+            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D;
+#pragma unroll
+            for (int i = 0; i < UPL; ++i) {
+                const int u = lane + 64 * i, d = u % D, j = u / D;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    x[i][e] = base[(size_t)kv_of_slot_f16(8 * j + e) * d_model + d];
+                    amax = fmaxf(amax, fabsf(x[i][e]));
+                }
+            }
+        }
+        amax = wave_max64(amax);
+        const float sc = qmha_scale_from_absmax(amax);
+        const float inv = 1.0f / sc;
+        if (active) {
+            _Float16* dst = static_cast<_Float16*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
+#pragma unroll
+            for (int i = 0; i < UPL; ++i) {
+                const int u = lane + 64 * i, d = u % D, j = u / D;
+                v8h h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (_Float16)qmha_quant_i8(x[i][e], inv);
+                *reinterpret_cast<v8h*>(dst + d * 32 + 8 * j) = h;
+            }
+            if (lane == 0) sV[item] = sc;
+        }
+        return;
+    }
+
     const int ri = lane / C4, ci = lane % C4;
     v4f v[NI];
     float amax = 0.0f;
