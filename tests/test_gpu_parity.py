@@ -165,6 +165,43 @@ def test_edge_values(dev, oracle_mod, variant):
     assert_parity(variant, out, ref, scale=4)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_growing_scores_reanchor(dev, oracle_mod, variant):
+    """Scores that climb by ~100 log2 units along the sequence: every tile raises the running
+    max, and the int8 kernel's anchored accumulator must re-anchor (m - anchor > 48)."""
+    N, dm, h = 512, 128, 2
+    rng = np.random.default_rng(7)
+    Q = (rng.standard_normal((N, dm)) * 0.2 + 1.0).astype(np.float32)
+    ramp = np.linspace(0.0, 4.0, N, dtype=np.float32)[:, None]
+    K = ((rng.standard_normal((N, dm)) * 0.2 + 1.0) * ramp).astype(np.float32)
+    V = rng.standard_normal((N, dm)).astype(np.float32)
+    out = run(variant, Q, K, V, dm, h, dev)
+    ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
+    # fp16: with a few dominant keys per row one exp2-vs-expf ulp can flip half(p) (2^-11
+    # relative) and move O by ~5e-4 |V|; bound by the reference's own 1e-3 verify tolerance
+    assert_parity(variant, out, ref, scale=5.0 if variant == "fa_tc_v1a" else 1.0)
+
+
+@pytest.mark.parametrize("variant", ["fa_tc_int8_b", "fa_tc_v1a", "fa"])
+def test_underflow_guard_and_zero_v(dev, oracle_mod, variant):
+    """m0 = 0 (fa_tc_int8_b.cu:402): with all scores far below 0 the row sum underflows past the
+    guard (1e-20 int8, 1e-10 fp16/fp32, fa_tc_int8_b.cu:549-553) and the reference writes 0.
+    (The unfused path runs a max-subtracted row softmax, unfused.cu, and has no such guard.)"""
+    N, dm, h = 128, 128, 2
+    rng = np.random.default_rng(8)
+    Q = np.full((N, dm), 3.0, np.float32)
+    K = np.full((N, dm), -3.0, np.float32) + (rng.standard_normal((N, dm)) * 0.01).astype(np.float32)
+    V = rng.standard_normal((N, dm)).astype(np.float32)
+    out = run(variant, Q, K, V, dm, h, dev)
+    ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
+    assert np.array_equal(ref, np.zeros_like(ref))  # the oracle takes the guard
+    assert np.array_equal(out, np.zeros_like(out))
+    # V == 0: any finite attention is exactly 0
+    Q, K = (rng.standard_normal((N, dm)).astype(np.float32) for _ in range(2))
+    out = run(variant, Q, K, np.zeros((N, dm), np.float32), dm, h, dev)
+    assert np.array_equal(out, np.zeros_like(out))
+
+
 def test_deterministic(dev):
     Q, K, V = rand_inputs(5, 2, 512, 256)
     a = run("fa_tc_int8_b", Q, K, V, 256, 4, dev)
