@@ -480,7 +480,7 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
 template <int D, int WAVES, int FL>
-__global__ __launch_bounds__(WAVES * 64, 2) void qmha_fa_int8_pipe_kernel(
+__global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int8_pipe_kernel(
     const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sQ, const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
