@@ -202,7 +202,7 @@ __device__ __forceinline__ int chunk_swz(int row) {
 // ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
 //   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4 };
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -590,13 +590,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
         // operand reads for this iteration's MFMAs
         v8h v00, v01, v10, v11;
         v4i k0, k1;
-        if constexpr (has_prev) {
+        constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
+        if constexpr (has_prev && !JIT) {
             v00 = vop_of(t - 1, 0, 0);
             v10 = vop_of(t - 1, 1, 0);
             v01 = vop_of(t - 1, 0, 1);
             v11 = vop_of(t - 1, 1, 1);
         }
-        if constexpr (has_next) {
+        if constexpr (has_next && !JIT) {
             k0 = kop_of(t + 1, 0);
             k1 = kop_of(t + 1, 1);
         }
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
         const float m_new = fmaxf(m_run, mx * c);
         const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
         QMHA_FENCE();
-        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v00, pp0, v16f{}, 0, 0, 0);
+        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0);
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = fmaxf(div127_fast(pmax), 1e-8f);
@@ -621,7 +622,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
             x[r] = fmaf(sv, c, -m_new);
         }
         QMHA_FENCE();
-        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v10, pp0, v16f{}, 0, 0, 0);
+        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 0) : v10, pp0, v16f{}, 0, 0, 0);
         QMHA_FENCE();
         // ---- C: scores of rows 8..15
 #pragma unroll
@@ -630,20 +631,20 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
             x[r] = fmaf(sv, c, -m_new);
         }
         QMHA_FENCE();
-        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v01, pp1, a0, 0, 0, 0);
+        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 1) : v01, pp1, a0, 0, 0, 0);
         QMHA_FENCE();
         // ---- D: p = exp2, rows 0..7
         float p[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k0, qop[0], magic_blk, 0, 0, 0);
+        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(JIT ? kop_of(t + 1, 0) : k0, qop[0], magic_blk, 0, 0, 0);
         QMHA_FENCE();
         // ---- E: p = exp2, rows 8..15
 #pragma unroll
         for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v11, pp1, a1, 0, 0, 0);
+        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 1) : v11, pp1, a1, 0, 0, 0);
         QMHA_FENCE();
         // ---- F: Pi = rint(p/sP) as exact f16 integers
 #pragma unroll
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
             }
         }
         QMHA_FENCE();
-        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k1, qop[1], s_nxt, 0, 0, 0);
+        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(JIT ? kop_of(t + 1, 1) : k1, qop[1], s_nxt, 0, 0, 0);
         QMHA_FENCE();
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         const float rs = half_swap_add(tree_sum16(p));
@@ -843,6 +844,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, float* O, int B, int N, int 
             case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, O, B, N, H, d_model, stream);
             case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, O, B, N, H, d_model, stream);
             case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, O, B, N, H, d_model, stream);
+            case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, O, B, N, H, d_model, stream);
             default: break;
         }
         // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
