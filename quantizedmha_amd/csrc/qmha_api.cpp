@@ -193,7 +193,7 @@ qmha::Int8Workspace int8_slice(const qmha::Int8Workspace& w, size_t b0, int N, i
 }
 qmha::F16Workspace f16_slice(const qmha::F16Workspace& w, size_t b0, int N, int H, int D) {
     const size_t e = b0 * H * N * D;
-    return qmha::F16Workspace{w.Qh + e, w.Kh + e, w.Vt + e};
+    return qmha::F16Workspace{nullptr, w.Kh + e, w.Vt + e};
 }
 
 int run(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model, int h, int variant,
@@ -252,7 +252,7 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             if (variant == QMHA_FA_TC_INT8_B) {
                 const qmha::Int8Workspace w = int8_slice(w8, b0, N, h, D);
                 QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, 1, nb, N, h, D,
-                                                     d_model, pre_s), "quant_int8 launch");
+                                                     d_model, pre_s, /*first_tensor=*/1), "quant_int8 launch");
             } else {
                 QMHA_HIP_TRY(qmha::launch_convert_f16(Q + b0 * slab, K + b0 * slab, V + b0 * slab, f16_slice(w16, b0, N, h, D),
                                                       nb, N, h, D, d_model, pre_s), "convert_f16 launch");
@@ -265,11 +265,11 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             if (nc > 1) QMHA_HIP_TRY(hipStreamWaitEvent(stream, side->ready[c], 0), "hipStreamWaitEvent");
             QMHA_MARK(rec.main, stream, true);
             if (variant == QMHA_FA_TC_INT8_B) {
-                QMHA_HIP_TRY(qmha::launch_fa_int8_main(int8_slice(w8, b0, N, h, D), O + b0 * slab, nb, N, h, D, d_model, stream),
-                             "fa_int8 launch");
+                QMHA_HIP_TRY(qmha::launch_fa_int8_main(int8_slice(w8, b0, N, h, D), Q + b0 * slab, O + b0 * slab, nb, N, h, D,
+                                                       d_model, stream), "fa_int8 launch");
             } else {
-                QMHA_HIP_TRY(qmha::launch_fa_f16_main(f16_slice(w16, b0, N, h, D), O + b0 * slab, nb, N, h, D, d_model, stream),
-                             "fa_f16 launch");
+                QMHA_HIP_TRY(qmha::launch_fa_f16_main(f16_slice(w16, b0, N, h, D), Q + b0 * slab, O + b0 * slab, nb, N, h, D,
+                                                      d_model, stream), "fa_f16 launch");
             }
             QMHA_MARK(rec.main, stream, false);
         }

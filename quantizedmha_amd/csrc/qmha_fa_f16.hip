@@ -22,9 +22,9 @@ template <int D>
 __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     _Float16* __restrict__ Qh, _Float16* __restrict__ Kh, _Float16* __restrict__ Vt,
-    int N, int H, int d_model, int total_groups) {
+    int N, int H, int d_model, int total_groups, int first_tensor) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
-    const int tensor = blockIdx.y;
+    const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int item = blockIdx.x * 4 + wave;
     const bool active = item < total_groups;
@@ -76,198 +76,8 @@ __device__ __forceinline__ int chunk_swz_h(int row) {
     return (row / rpb) & (RB / 16 - 1);
 }
 
-template <int D, int WAVES, int SG = 2>
-__global__ __launch_bounds__(WAVES * 64) void qmha_fa_f16_kernel(
-    const _Float16* __restrict__ Qh, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
-    static_assert(SG == 2, "the stage is processed as one interleaved pair of tiles");
-    constexpr int KS = D / 16;   // QK k-steps (K = 16)
-    constexpr int MB = D / 32;   // PV d-blocks
-    constexpr int RB = 2 * D;    // K row bytes
-    constexpr int STAGE_BYTES = SG * 32 * D * 2;
-    constexpr int NT = WAVES * 64;
-    constexpr int CH = STAGE_BYTES / 16;
-    constexpr int CPT = (CH + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) char lds[2][2 * STAGE_BYTES];
-
-    const int G = N / QMHA_GROUP;
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = wg / nqb, qb = wg % nqb;
-    const int b = bh / H, k = bh % H;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int qg = qb * WAVES + wave;
-    const bool active = qg < G;
-    const int half = lane >> 5, col = lane & 31;
-
-    v8h qop[KS];
-    if (active) {
-        const _Float16* qp = Qh + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 8 * half;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) qop[s] = *reinterpret_cast<const v8h*>(qp + 16 * s);
-    } else {
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) qop[s][e] = (_Float16)0.0f;
-    }
-    v16f o[MB];
-#pragma unroll
-    for (int m = 0; m < MB; ++m)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[m][r] = 0.0f;
-    float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290)
-
-    const char* kbase = reinterpret_cast<const char*>(Kh + (size_t)bh * N * D);
-    const char* vbase = reinterpret_cast<const char*>(Vt + (size_t)bh * N * D);
-    const int nst = (G + SG - 1) / SG;
-    v4i kst[CPT], vst[CPT];
-    auto gload = [&](int st) {
-        const int g0 = st * SG;
-        const int nch = min(SG, G - g0) * 32 * D * 2 / 16;
-        const v4i* ks = reinterpret_cast<const v4i*>(kbase + (size_t)g0 * 32 * D * 2);
-        const v4i* vs = reinterpret_cast<const v4i*>(vbase + (size_t)g0 * 32 * D * 2);
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int idx = tid + c * NT;
-            if (idx < nch) {
-                kst[c] = ks[idx];
-                vst[c] = vs[idx];
-            }
-        }
-    };
-    auto lstore = [&](int buf, int st) {
-        const int g0 = st * SG;
-        const int nch = min(SG, G - g0) * 32 * D * 2 / 16;
-        char* L = lds[buf];
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int idx = tid + c * NT;
-            if (idx < nch) {
-                const int row = idx / (RB / 16), cc = idx % (RB / 16);
-                *reinterpret_cast<v4i*>(L + row * RB + 16 * (cc ^ chunk_swz_h<RB>(row))) = kst[c];
-                const int grp = idx / (4 * D), w = idx % (4 * D);  // V rows are 64 B = 4 chunks
-                const int d = w >> 2, cv = w & 3;
-                *reinterpret_cast<v4i*>(L + STAGE_BYTES + grp * 64 * D + d * 64 + 16 * (cv ^ chunk_swz_h<64>(d))) = vst[c];
-            }
-        }
-    };
-
-    // S^T = K Q^T (f32 accumulate) of tile gi of the stage in LDS
-    auto qk = [&](const char* L, int gi) {
-        v16f s = {};
-        const int krow = gi * 32 + col;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
-            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
-        }
-        return s;
-    };
-    auto rowmax = [&](const v16f& s) {
-        float a = fmaxf(fmaxf(s[0], s[1]), s[2]), b = fmaxf(fmaxf(s[3], s[4]), s[5]);
-        float c = fmaxf(fmaxf(s[6], s[7]), s[8]), d = fmaxf(fmaxf(s[9], s[10]), s[11]);
-        float e = fmaxf(fmaxf(s[12], s[13]), s[14]);
-        return half_swap_max(fmaxf(fmaxf(fmaxf(a, b), fmaxf(c, d)), fmaxf(e, s[15])));
-    };
-    // P = half(exp(s - m)) as the two k-step operands; rs = sum of the fp32 p (fa_tc_v1a.cu:169-174)
-    auto ptile = [&](const v16f& s, float m, v8h* pop, float& rs) {
-        float p[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m));
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            const v2h h2 = __builtin_convertvector((v2f{p[r], p[r + 1]}), v2h);  // v_cvt_pk_f16_f32 (RNE)
-            pop[r >> 3][r & 7] = h2[0];
-            pop[r >> 3][(r & 7) + 1] = h2[1];
-        }
-        rs = tree_sum16(p);
-    };
-    auto rescale = [&](float a) {
-        if (__builtin_amdgcn_ballot_w64(a != 1.0f)) {
-#pragma unroll
-            for (int m = 0; m < MB; ++m)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] *= a;
-        }
-    };
-    // O^T += V^T P^T with the fp32 accumulator as the MFMA C operand (fa_tc_v1a.cu:218)
-    auto pv = [&](const char* L, int gi, const v8h* pop) {
-#pragma unroll
-        for (int m = 0; m < MB; ++m) {
-            const int d = 32 * m + col;
-            const char* vr = L + STAGE_BYTES + gi * 64 * D + d * 64;
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
-                o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
-            }
-        }
-    };
-
-    gload(0);
-    lstore(0, 0);
-    qmha_dma_barrier();
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        if (st + 1 < nst) gload(st + 1);
-        if (active) {
-            const int t0 = st * SG;
-            const char* L = lds[buf];
-            if (t0 + 1 < G) {
-                // interleaved pair; the running max is chained per 32-key tile (:286-303)
-                const v16f s0 = qk(L, 0);
-                const v16f s1 = qk(L, 1);
-                const float m1 = fmaxf(m_run, rowmax(s0) * c_log2);
-                const float m2 = fmaxf(m1, rowmax(s1) * c_log2);
-                const float a1 = __builtin_amdgcn_exp2f(m_run - m1);  // :195
-                const float a2 = __builtin_amdgcn_exp2f(m1 - m2);
-                v8h p0[2], p1[2];
-                float rs0, rs1;
-                ptile(s0, m1, p0, rs0);
-                ptile(s1, m2, p1, rs1);
-                rs0 = half_swap_add(rs0);
-                rs1 = half_swap_add(rs1);
-                l_run = fmaf(a2, fmaf(a1, l_run, rs0), rs1);  // :198 twice
-                m_run = m2;
-                rescale(a1);  // :207
-                pv(L, 0, p0);
-                rescale(a2);
-                pv(L, 1, p1);
-            } else {
-                const v16f s0 = qk(L, 0);
-                const float m1 = fmaxf(m_run, rowmax(s0) * c_log2);
-                const float a1 = __builtin_amdgcn_exp2f(m_run - m1);
-                v8h p0[2];
-                float rs0;
-                ptile(s0, m1, p0, rs0);
-                rs0 = half_swap_add(rs0);
-                l_run = fmaf(a1, l_run, rs0);
-                m_run = m1;
-                rescale(a1);
-                pv(L, 0, p0);
-            }
-        }
-        if (st + 1 < nst) lstore(buf ^ 1, st + 1);
-        qmha_dma_barrier();
-    }
-    if (active) {
-        const bool ok = l_run > 1e-10f;
-        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
-#pragma unroll
-        for (int m = 0; m < MB; ++m)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                v4f w;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = ok ? o[m][4 * g4 + j] / l_run : 0.0f;
-                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
-            }
-    }
-}
-
 // ---------------------------------------------------------------------------------------
-// Main kernel v2: K/V staged by LDS-DMA (global_load_lds, swizzled source / linear LDS image),
+// Main kernel: K/V staged by LDS-DMA (global_load_lds, swizzled source / linear LDS image),
 // one 32-key tile at a time, Q@K^T of the next tile issued before the current softmax
 // (FL_PREFETCH).  One wave = one 32-row Q group.
 // ---------------------------------------------------------------------------------------
@@ -275,7 +85,7 @@ enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4 };
 
 template <int D, int WAVES, int SG, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f16_v2_kernel(
-    const _Float16* __restrict__ Qh, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
+    const float* __restrict__ Qf, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     QMHA_ENABLE_AGPR_MFMA();
     constexpr int KS = D / 16;           // QK k-steps (K = 16)
@@ -299,9 +109,18 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
 
     v8h qop[KS];
     if (active) {
-        const _Float16* qp = Qh + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 8 * half;
+        // Q converted in-kernel (RNE, __float2half) straight into the operand: elements
+        // [16 s + 8 half, +8) of query row col (saves the pre-pass its Q traffic)
+        const float* qp = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 8 * half;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) qop[s] = *reinterpret_cast<const v8h*>(qp + 16 * s);
+        for (int s = 0; s < KS; ++s) {
+            const v4f a = *reinterpret_cast<const v4f*>(qp + 16 * s), c = *reinterpret_cast<const v4f*>(qp + 16 * s + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                qop[s][e] = (_Float16)a[e];
+                qop[s][4 + e] = (_Float16)c[e];
+            }
+        }
     } else {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -459,16 +278,16 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
 }
 
 size_t f16_workspace_bytes(int B, int N, int H, int D) {
-    return 3 * align_up((size_t)B * H * N * D * 2, 256);
+    return 2 * align_up((size_t)B * H * N * D * 2, 256);  // Kh, Vt (Q is converted in the main kernel)
 }
 
 F16Workspace f16_carve(void* ws, int B, int N, int H, int D) {
     const size_t e = align_up((size_t)B * H * N * D * 2, 256);
     char* p = static_cast<char*>(ws);
     F16Workspace w;
-    w.Qh = reinterpret_cast<_Float16*>(p);
-    w.Kh = reinterpret_cast<_Float16*>(p + e);
-    w.Vt = reinterpret_cast<_Float16*>(p + 2 * e);
+    w.Qh = nullptr;
+    w.Kh = reinterpret_cast<_Float16*>(p);
+    w.Vt = reinterpret_cast<_Float16*>(p + e);
     return w;
 }
 
@@ -476,8 +295,9 @@ template <int D>
 static hipError_t convert_f16_d(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
                                 int H, int d_model, hipStream_t stream) {
     const int total = B * H * (N / QMHA_GROUP);
-    hipLaunchKernelGGL((qmha_convert_f16_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.Qh,
-                       w.Kh, w.Vt, N, H, d_model, total);
+    // K and V only: the main kernel converts Q itself (blockIdx.y = tensor - 1)
+    hipLaunchKernelGGL((qmha_convert_f16_kernel<D>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V, w.Qh,
+                       w.Kh, w.Vt, N, H, d_model, total, 1);
     return hipGetLastError();
 }
 
@@ -491,58 +311,46 @@ hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, co
     }
 }
 
-template <int D, int WAVES, int SG>
-static hipError_t fa_f16_launch(const F16Workspace& w, float* O, int B, int N, int H, int d_model,
-                                hipStream_t stream) {
-    const int G = N / QMHA_GROUP;
-    const int nqb = (G + WAVES - 1) / WAVES;
-    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;  // fa_tc_v1a.cu:421
-    hipLaunchKernelGGL((qmha_fa_f16_kernel<D, WAVES, SG>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qh, w.Kh,
-                       w.Vt, O, N, H, d_model, nqb, c_log2);
-    return hipGetLastError();
-}
-
 template <int D, int WAVES, int SG, int FL>
-static hipError_t fa_f16_v2_launch(const F16Workspace& w, float* O, int B, int N, int H, int d_model,
+static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                                    hipStream_t stream) {
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;
-    hipLaunchKernelGGL((qmha_fa_f16_v2_kernel<D, WAVES, SG, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qh,
+    hipLaunchKernelGGL((qmha_fa_f16_v2_kernel<D, WAVES, SG, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
                        w.Kh, w.Vt, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
 
 template <int D>
-static hipError_t fa_f16_d(const F16Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
+static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                           hipStream_t stream) {
     if constexpr (D == 64) {
         switch (tune_config("QMHA_F16_CFG")) {
-            case 82: return fa_f16_launch<D, 8, 2>(w, O, B, N, H, d_model, stream);
-            case 22: return fa_f16_launch<D, 2, 2>(w, O, B, N, H, d_model, stream);
-            case 420: return fa_f16_v2_launch<D, 4, 2, 0>(w, O, B, N, H, d_model, stream);
-            case 421: return fa_f16_v2_launch<D, 4, 2, F16_PREFETCH>(w, O, B, N, H, d_model, stream);
-            case 440: return fa_f16_v2_launch<D, 4, 4, 0>(w, O, B, N, H, d_model, stream);
-            case 441: return fa_f16_v2_launch<D, 4, 4, F16_PREFETCH>(w, O, B, N, H, d_model, stream);
-            case 424: return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, O, B, N, H, d_model, stream);
-            case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, O, B, N, H, d_model, stream);
+            case 420: return fa_f16_v2_launch<D, 4, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 421: return fa_f16_v2_launch<D, 4, 2, F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 440: return fa_f16_v2_launch<D, 4, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 441: return fa_f16_v2_launch<D, 4, 4, F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 424: return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
 #ifdef QMHA_ABLATION
-            case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, O, B, N, H, d_model, stream);
-            case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, O, B, N, H, d_model, stream);
+            case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, Qf, O, B, N, H, d_model, stream);
 #endif
             default: break;
         }
     }
     // default: v2 (LDS-DMA staging, per-tile softmax), 4 waves/SIMD budget (r01 A/B: 1.54 ms vs
     // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64)
-    return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, O, B, N, H, d_model, stream);
+    return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
 }
 
-hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,
+hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,
                               hipStream_t stream) {
     switch (D) {
-        case 32: return fa_f16_d<32>(w, O, B, N, H, d_model, stream);
-        case 64: return fa_f16_d<64>(w, O, B, N, H, d_model, stream);
-        case 128: return fa_f16_d<128>(w, O, B, N, H, d_model, stream);
+        case 32: return fa_f16_d<32>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_f16_d<64>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_f16_d<128>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -48,13 +48,13 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int v_mode) {
+    int N, int H, int d_model, int total_groups, int v_mode, int first_tensor) {
     constexpr int C4 = D / 4;        // float4 per row
     constexpr int RPI = 64 / C4;     // rows per load instruction
     constexpr int NI = 32 / RPI;     // load instructions per lane
     __shared__ __attribute__((aligned(16))) _Float16 vtile[4][32 * D];
 
-    const int tensor = blockIdx.y;
+    const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int item = blockIdx.x * 4 + wave;  // (bh, g)
@@ -182,6 +182,38 @@ __device__ __forceinline__ int chunk_swz(int row) {
     return (row / rows_per_bankrow) & (cpr - 1);
 }
 
+// In-kernel Q quantisation (fa_tc_int8_b.cu:33-152, the pre-pass arithmetic) straight into
+// the Q^T MFMA operand: lane (col, half) loads the D/2 values of query row `col` it feeds to
+// the i8 MFMA (bytes [32 s + 16 half, +16) of every k-step s), the wave reduces the group's
+// absmax.  Returns the group scale sQ.  Saves the pre-pass a third of its HBM traffic.
+template <int D>
+__device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, int half, v4i (&qop)[D / 32]) {
+    constexpr int KS = D / 32;
+    v4f x[KS][4];
+    float amax = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            x[s][c4] = *reinterpret_cast<const v4f*>(row + 32 * s + 16 * half + 4 * c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(x[s][c4][e]));
+        }
+    amax = wave_max64(amax);
+    const float sc = qmha_scale_from_absmax(amax);
+    const float inv = 1.0f / sc;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w |= ((uint32_t)(uint8_t)qmha_quant_i8(x[s][c4][e], inv)) << (8 * e);
+            qop[s][c4] = (int)w;
+        }
+    return sc;
+}
+
 // ---------------------------------------------------------------------------------------
 // Main kernel.
 //
@@ -206,8 +238,8 @@ enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
-    const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
-    const float* __restrict__ sQ, const float* __restrict__ sK, const float* __restrict__ sV,
+    const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     constexpr int KS = D / 32;                    // i8 MFMA k-steps (QK) and d-blocks (PV)
     constexpr int KBYTES = SG * 32 * D;           // K int8 per stage
@@ -237,10 +269,8 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
     for (int j = 0; j < QPW; ++j) {
         const int qg = (qb * WAVES + wave) * QPW + j;
         if (qg < G) {  // wave-uniform
-            const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
-#pragma unroll
-            for (int s = 0; s < KS; ++s) qop[j][s] = *reinterpret_cast<const v4i*>(qp + 32 * s);
-            cq[j] = sQ[(size_t)bh * G + qg] * c_log2;
+            const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
+            cq[j] = quant_q_operand<D>(qrow, half, qop[j]) * c_log2;
         } else {  // padding group: computes on a zero Q, never stored
 #pragma unroll
             for (int s = 0; s < KS; ++s) qop[j][s] = v4i{0, 0, 0, 0};
@@ -481,8 +511,8 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // ---------------------------------------------------------------------------------------
 template <int D, int WAVES, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int8_pipe_kernel(
-    const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
-    const float* __restrict__ sQ, const float* __restrict__ sK, const float* __restrict__ sV,
+    const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     static_assert(D == 64, "pipelined schedule is written for d = 64 (2 k-steps, 2 d-blocks)");
     constexpr int SG = 2, RING = 3;
@@ -507,10 +537,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
     v4i qop[2];
     float cq = 0.0f;
     if (active) {
-        const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
-        qop[0] = *reinterpret_cast<const v4i*>(qp);
-        qop[1] = *reinterpret_cast<const v4i*>(qp + 32);
-        cq = sQ[(size_t)bh * G + qg] * c_log2;
+        const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
+        cq = quant_q_operand<D>(qrow, half, qop) * c_log2;
     } else {
         qop[0] = qop[1] = v4i{0, 0, 0, 0};
     }
@@ -777,88 +805,89 @@ Int8Workspace int8_carve(void* ws, int B, int N, int H, int D) {
 
 template <int D>
 static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                               int v_mode, int B, int N, int H, int d_model, hipStream_t stream) {
+                               int v_mode, int B, int N, int H, int d_model, int first_tensor, hipStream_t stream) {
     const int total = B * H * (N / QMHA_GROUP);
-    dim3 grid((total + 3) / 4, 3);
+    dim3 grid((total + 3) / 4, 3 - first_tensor);
     hipLaunchKernelGGL((qmha_quant_int8_kernel<D>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ, w.sK,
-                       w.sV, N, H, d_model, total, v_mode);
+                       w.sV, N, H, d_model, total, v_mode, first_tensor);
     return hipGetLastError();
 }
 
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream) {
+                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream, int first_tensor) {
     switch (D) {
-        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, stream);
-        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, stream);
-        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, stream);
+        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
+        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
+        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL = 0>
-static hipError_t fa_int8_launch(const Int8Workspace& w, float* O, int B, int N, int H, int d_model,
+static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                                  hipStream_t stream) {
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES * QPW - 1) / (WAVES * QPW);
     const int nwg = B * H * nqb;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;  // inv_sqrt_d: fa_tc_int8_b.cu:587
-    hipLaunchKernelGGL((qmha_fa_int8_kernel<D, WAVES, QPW, SG, FL, ABL>), dim3(nwg), dim3(WAVES * 64), 0, stream, w.Qi,
-                       w.Ki, w.Vh, w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+    hipLaunchKernelGGL((qmha_fa_int8_kernel<D, WAVES, QPW, SG, FL, ABL>), dim3(nwg), dim3(WAVES * 64), 0, stream, Qf,
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
 
 template <int D, int WAVES, int FL>
-static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, float* O, int B, int N, int H, int d_model,
-                                      hipStream_t stream) {
+static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
+                                      int d_model, hipStream_t stream) {
     const int G = N / QMHA_GROUP;
-    if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);  // no pipeline to fill
+    if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
-    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, w.Qi,
-                       w.Ki, w.Vh, w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
 
 // Default geometry per head size, and the QMHA_INT8_CFG tuning alternatives (profiling).
 template <int D>
-static hipError_t fa_int8_d(const Int8Workspace& w, float* O, int B, int N, int H, int d_model, hipStream_t stream) {
+static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                            hipStream_t stream) {
     if constexpr (D == 64) {
 #ifdef QMHA_ABLATION
         static const int abl = std::getenv("QMHA_INT8_ABL") ? std::atoi(std::getenv("QMHA_INT8_ABL")) : 0;
         switch (abl) {
-            case 1: return fa_int8_launch<D, 4, 1, 2, 0, 1>(w, O, B, N, H, d_model, stream);
-            case 2: return fa_int8_launch<D, 4, 1, 2, 0, 2>(w, O, B, N, H, d_model, stream);
-            case 4: return fa_int8_launch<D, 4, 1, 2, 0, 4>(w, O, B, N, H, d_model, stream);
-            case 16: return fa_int8_launch<D, 4, 1, 2, 0, 16>(w, O, B, N, H, d_model, stream);
-            case 64: return fa_int8_launch<D, 4, 1, 2, 0, 64>(w, O, B, N, H, d_model, stream);
-            case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, O, B, N, H, d_model, stream);
-            case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, O, B, N, H, d_model, stream);
-            case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, O, B, N, H, d_model, stream);
+            case 1: return fa_int8_launch<D, 4, 1, 2, 0, 1>(w, Qf, O, B, N, H, d_model, stream);
+            case 2: return fa_int8_launch<D, 4, 1, 2, 0, 2>(w, Qf, O, B, N, H, d_model, stream);
+            case 4: return fa_int8_launch<D, 4, 1, 2, 0, 4>(w, Qf, O, B, N, H, d_model, stream);
+            case 16: return fa_int8_launch<D, 4, 1, 2, 0, 16>(w, Qf, O, B, N, H, d_model, stream);
+            case 64: return fa_int8_launch<D, 4, 1, 2, 0, 64>(w, Qf, O, B, N, H, d_model, stream);
+            case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, Qf, O, B, N, H, d_model, stream);
+            case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, Qf, O, B, N, H, d_model, stream);
+            case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
         switch (tune_config("QMHA_INT8_CFG")) {
-            case 4120: return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);
-            case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, O, B, N, H, d_model, stream);
-            case 4125: return fa_int8_launch<D, 4, 1, 2, FL_MAGIC | FL_LB2>(w, O, B, N, H, d_model, stream);
-            case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, O, B, N, H, d_model, stream);
-            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, O, B, N, H, d_model, stream);
-            case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, O, B, N, H, d_model, stream);
-            case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, O, B, N, H, d_model, stream);
+            case 4120: return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 4125: return fa_int8_launch<D, 4, 1, 2, FL_MAGIC | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
+            case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
         // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
-        return fa_int8_pipe_launch<D, 4, 0>(w, O, B, N, H, d_model, stream);
+        return fa_int8_pipe_launch<D, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
     }
-    return fa_int8_launch<D, 4, 1, 2, 0>(w, O, B, N, H, d_model, stream);
+    return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
 }
 
-hipError_t launch_fa_int8_main(const Int8Workspace& w, float* O, int B, int N, int H, int D, int d_model,
-                               hipStream_t stream) {
+hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, hipStream_t stream) {
     switch (D) {
-        case 32: return fa_int8_d<32>(w, O, B, N, H, d_model, stream);
-        case 64: return fa_int8_d<64>(w, O, B, N, H, d_model, stream);
-        case 128: return fa_int8_d<128>(w, O, B, N, H, d_model, stream);
+        case 32: return fa_int8_d<32>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_d<64>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_d<128>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -26,15 +26,18 @@ struct Int8Workspace {
 size_t int8_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
+// first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream);
-hipError_t launch_fa_int8_main(const Int8Workspace& w, float* O, int B, int N, int H, int D, int d_model,
-                               hipStream_t stream);
+                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream,
+                             int first_tensor = 0);
+// Qf: the caller's fp32 Q (the main kernel quantises each Q group into its MFMA operand)
+hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, hipStream_t stream);
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream);
 
 // ---- FP16 (fa_tc_v1a) ------------------------------------------------------------------
 struct F16Workspace {
-    _Float16* Qh;  // [B*H][N][D]
+    _Float16* Qh;  // unused (nullptr): the main kernel converts Q in registers
     _Float16* Kh;  // [B*H][N][D]
     _Float16* Vt;  // [B*H][N/32][D][32]  (f16 operand slot order)
 };
@@ -42,7 +45,7 @@ size_t f16_workspace_bytes(int B, int N, int H, int D);
 F16Workspace f16_carve(void* ws, int B, int N, int H, int D);
 hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
                               int H, int D, int d_model, hipStream_t stream);
-hipError_t launch_fa_f16_main(const F16Workspace& w, float* O, int B, int N, int H, int D, int d_model,
+hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,
                               hipStream_t stream);
 
 // ---- FP32 scalar (fa) ------------------------------------------------------------------
