@@ -6,11 +6,11 @@
 //   P stored as half(p) (:174);  O = alpha*O + Ph Vh (fp32 accumulate, :218)
 //   out = O / l, 0 if l <= 1e-10 (:384-388)
 //
-// Same skeleton as the INT8 kernel: a conversion pre-pass writes Q/K as f16 rows and V in
-// the f16 V^T operand order; the main kernel keeps Q in registers, streams K/V tiles
-// through double-buffered swizzled LDS and runs both products on v_mfma_f32_32x32x16_f16
-// with swapped operands.  The O accumulator is the MFMA C operand, so the P@V
-// accumulation costs no VALU; alpha == 1 rescales are skipped exactly.
+// Same skeleton as the INT8 kernel: a conversion pre-pass writes K as f16 rows and V in the
+// f16 V^T operand order; the main kernel converts its Q group into registers, streams K/V
+// tiles through LDS-DMA-filled swizzled LDS and runs both products on
+// v_mfma_f32_32x32x16_f16 with swapped operands.  The O accumulator is the MFMA C operand,
+// so the P@V accumulation costs no VALU; alpha == 1 rescales are skipped exactly.
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 

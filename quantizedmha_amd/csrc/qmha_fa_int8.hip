@@ -9,23 +9,24 @@
 //   O = alpha*O + (Pi Vi) * sP * sV,   out = O / l  (0 if l <= 1e-20)
 //
 // Two launches per call:
-//   1. qmha_quant_int8_kernel: reads fp32 Q/K/V once; writes int8 Q and K rows per head and
-//      the quantised V integers in the MFMA V^T operand order, one fp32 scale per group.
-//      Bit-identical to the reference quantiser (same fp32 ops, RNE rounding).
-//   2. qmha_fa_int8_kernel: one workgroup = WAVES waves = WAVES*32 query rows of one head;
-//      each wave owns exactly one 32-row Q group (= one Q quantisation group).  K/V tiles
-//      stream HBM -> registers -> LDS (double buffered, XOR-swizzled, conflict-free
-//      ds_read_b128).  Both products use swapped operands (S^T = K Q^T, O^T = V^T P^T) so
-//      every query's statistics are lane-local and P^T feeds the second MFMA from registers.
+//   1. qmha_quant_int8_kernel: reads fp32 K/V once; writes int8 K rows per head and the
+//      quantised V integers in the MFMA V^T operand order, one fp32 scale per group.
+//      Bit-identical to the reference quantiser (same fp32 ops, RNE rounding).  (With Q too
+//      for qmha_quantize_int8 and the int32 Q@K^T test hook.)
+//   2. qmha_fa_int8_pipe_kernel (d = 64; qmha_fa_int8_kernel otherwise): one workgroup = 4
+//      waves = 128 query rows of one head; each wave owns one 32-row Q group, quantises it
+//      in registers (the same arithmetic) and sweeps all KV groups.  K/V tiles stream
+//      L2 -> LDS by LDS-DMA (XOR-swizzled image, conflict-free ds_read_b128).  Both products
+//      use swapped operands (S^T = K Q^T, O^T = V^T P^T) so every query's statistics are
+//      lane-local and P^T feeds the second MFMA from registers.
 //        Q@K^T: v_mfma_i32_32x32x32_i8, exact int32 scores.
 //        P@V  : the int8-valued operands Pi in [0,127], Vi in [-128,127] run on
 //               v_mfma_f32_32x32x16_f16.  Both are exact in f16, every product and every
 //               partial sum (|sum| <= 32*127*128 < 2^24) is exact in the fp32 accumulator,
 //               so the result equals the reference's int32 (Pi Vi) bit for bit -- but it
-//               arrives as fp32, saving the 32 int->float conversions per lane per tile
-//               that dominate an int32 epilogue (VALU is this kernel's bound).
-//      Software pipelining: the Q@K^T MFMAs of tile t+1 are issued before the softmax of
-//      tile t, so the matrix pipe runs under the VALU work of the same wave.
+//               arrives as fp32, saving the 32 int->float conversions per lane per tile.
+//      Software pipelining: P@V of tile t-1 and Q@K^T of tile t+1 are issued between the
+//      softmax chunks of tile t.
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
