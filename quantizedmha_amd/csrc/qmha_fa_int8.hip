@@ -44,16 +44,16 @@ static constexpr float kLog2e = 1.4426950408889634f;
 // v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
 // v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
 // ---------------------------------------------------------------------------------------
-template <int D>
+template <int D, int VMODE>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int v_mode, int first_tensor) {
+    int N, int H, int d_model, int total_groups, int first_tensor) {
+    constexpr int v_mode = VMODE;
     constexpr int C4 = D / 4;        // float4 per row
     constexpr int RPI = 64 / C4;     // rows per load instruction
     constexpr int NI = 32 / RPI;     // load instructions per lane
-    __shared__ __attribute__((aligned(16))) _Float16 vtile[4][32 * D];
 
     const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
@@ -131,9 +131,11 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
             }
             if (lane == 0) (tensor == 0 ? sQ : sK)[item] = sc;
         }
-    } else if (v_mode == 0) {
-        // int8 [D][32] with the i8 operand slot permutation, transposed through LDS
-        int8_t* tile = reinterpret_cast<int8_t*>(vtile[wave]);
+    } else if constexpr (v_mode == 0) {
+        // int8 [D][32] with the i8 operand slot permutation, transposed through LDS (only for
+        // the standalone qmha_quantize_int8 op; the attention path uses VMODE 1 above)
+        __shared__ __attribute__((aligned(16))) int8_t vtile[4][32 * D];
+        int8_t* tile = vtile[wave];
         if (active) {
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
@@ -146,26 +148,6 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
         if (active) {
             int8_t* dst = static_cast<int8_t*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
             constexpr int CH = 32 * D / 16;
-#pragma unroll
-            for (int c = lane; c < CH; c += 64)
-                reinterpret_cast<v4i*>(dst)[c] = reinterpret_cast<const v4i*>(tile)[c];
-            if (lane == 0) sV[item] = sc;
-        }
-    } else {
-        // f16-valued integers [D][32] with the f16 operand slot permutation
-        _Float16* tile = vtile[wave];
-        if (active) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int slot = slot_of_kv_f16(i * RPI + ri);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (_Float16)qmha_quant_i8(v[i][c], inv);
-            }
-        }
-        qmha_dma_barrier();
-        if (active) {
-            _Float16* dst = static_cast<_Float16*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
-            constexpr int CH = 32 * D * 2 / 16;
 #pragma unroll
             for (int c = lane; c < CH; c += 64)
                 reinterpret_cast<v4i*>(dst)[c] = reinterpret_cast<const v4i*>(tile)[c];
@@ -809,8 +791,12 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
                                int v_mode, int B, int N, int H, int d_model, int first_tensor, hipStream_t stream) {
     const int total = B * H * (N / QMHA_GROUP);
     dim3 grid((total + 3) / 4, 3 - first_tensor);
-    hipLaunchKernelGGL((qmha_quant_int8_kernel<D>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ, w.sK,
-                       w.sV, N, H, d_model, total, v_mode, first_tensor);
+    if (v_mode == 0)
+        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 0>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
+                           w.sK, w.sV, N, H, d_model, total, first_tensor);
+    else
+        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
+                           w.sK, w.sV, N, H, d_model, total, first_tensor);
     return hipGetLastError();
 }
 
