@@ -40,6 +40,16 @@
 // address-space pointer types for __builtin_amdgcn_global_load_lds (LDS-DMA)
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
+// buffer resource word 3 on gfx9-family parts (raw buffer, 32-bit data format)
+#define QMHA_BUF_DWORD3 0x00020000
+
+// 16 bytes per lane from base + voff + soff (bytes; nrec = bytes addressable from base) into
+// LDS at dst (wave-uniform) + 16 * lane: buffer_load_dwordx4 ... lds.  Uniform base / nrec
+// keep the resource in SGPRs; reads past nrec return zeros.
+__device__ __forceinline__ void buffer_load_lds16(const void* base, int nrec, lptr_t dst, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nrec, QMHA_BUF_DWORD3),
+                                             dst, 16, voff, soff, 0, 0);
+}
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));

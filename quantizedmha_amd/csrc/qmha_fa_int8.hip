@@ -531,30 +531,37 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
     const float* svb = sV + (size_t)bh * G;
     const int nst = (G + SG - 1) / SG;
 
+    // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
+    // stage offset rides in soffset, so a stage costs no address arithmetic on the VALU
+    constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
+    int koff[KJ], voff[VJ];
+#pragma unroll
+    for (int jj = 0; jj < KJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
+        koff[jj] = row * D + 16 * cc;
+    }
+#pragma unroll
+    for (int jj = 0; jj < VJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int grp = idx / (4 * D), w = idx % (4 * D);
+        const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
+        voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
+    }
     auto issue = [&](int st) {
         const int ngr = min(SG, G - st * SG);
-        const int8_t* ksrc = kbase + (size_t)st * KBYTES;
-        const char* vsrc = vbase + (size_t)st * VBYTES;
         int8_t* L = lds[st % RING];
 #pragma unroll
-        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+        for (int jj = 0; jj < KJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
-                const int idx = inst * 64 + lane;
-                const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
-                __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * D + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
-            }
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
+                buffer_load_lds16(kbase, N * D, (lptr_t)(L + inst * 1024), koff[jj], st * KBYTES);
         }
 #pragma unroll
-        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+        for (int jj = 0; jj < VJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
-                const int idx = inst * 64 + lane;
-                const int grp = idx / (4 * D), w = idx % (4 * D);
-                const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
-                __builtin_amdgcn_global_load_lds((gptr_t)(vsrc + grp * 64 * D + d * 64 + 16 * cv),
-                                                 (lptr_t)(L + KBYTES + inst * 1024), 16, 0, 0);
-            }
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
+                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
     // operand reads of tile t from the ring
@@ -577,7 +584,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
 
     v16f o0 = {}, o1 = {};      // O^T, d-blocks 0 and 1 (anchored)
     float m_run = 0.0f;          // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
-    float l_run = 0.0f;          // l * 2^(anchor - m)
+    float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
     v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
@@ -657,12 +664,15 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
         QMHA_FENCE();
         if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 1) : v11, pp1, a1, 0, 0, 0);
         QMHA_FENCE();
-        // ---- F: Pi = rint(p/sP) as exact f16 integers
+        // ---- F: Pi = rint(p/sP) (:317-321), carried as the f16 subnormal Pi * 2^-24:
+        // fma(p, 1/sP, 1.5 * 2^23) rounds half-even to an integer whose float bits end in Pi,
+        // and those low 16 bits are exactly the f16 encoding of Pi * 2^-24; one byte permute
+        // packs two entries.  P@V then yields T * 2^-24 exactly (T < 2^20); the O scale
+        // carries the 2^24 back.
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const float q0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
-            const float q1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
-            const v2h h2 = __builtin_convertvector((v2f{q0, q1}), v2h);
+            const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
+            const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
             if (r < 4) {
                 pc0[2 * r] = h2[0];
                 pc0[2 * r + 1] = h2[1];
@@ -675,10 +685,11 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
         if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(JIT ? kop_of(t + 1, 1) : k1, qop[1], s_nxt, 0, 0, 0);
         QMHA_FENCE();
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
-        const float rs = half_swap_add(tree_sum16(p));
+        // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
+        const float rs = tree_sum16(p);
         l_run = fmaf(rs, e, l_run);
         m_run = m_new;
-        const float scale_t = sp * svb[t] * e;
+        const float scale_t = sp * svb[t] * e * 16777216.0f;  // 2^24: P entries are Pi * 2^-24
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
         if constexpr (has_prev) {
 #pragma unroll
@@ -724,7 +735,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
     if (active) {
         const float unanchor = __builtin_amdgcn_exp2f(anchor - m_run);
-        const float l = l_run * unanchor;
+        const float l = half_swap_add(l_run) * unanchor;
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
@@ -858,13 +869,13 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 4125: return fa_int8_launch<D, 4, 1, 2, FL_MAGIC | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
             case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
-            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
+            case 9040: return fa_int8_pipe_launch<D, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
         // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
-        return fa_int8_pipe_launch<D, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
+        return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
     }
     return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
 }

@@ -60,6 +60,11 @@ def header_deps():
     return deps
 
 
+# per-source flags: the int8 softmax is written as scalar fp32 chains on purpose; SLP-packing
+# them into v_pk_* needs register pairs the exp results do not land in (a v_mov per pair)
+FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize"]}
+
+
 def compile_one(src, extra=()):
     out = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o").replace(".cpp", ".o"))
     if extra:
@@ -67,7 +72,7 @@ def compile_one(src, extra=()):
     full = os.path.join(CSRC, src)
     if newer(out, [full] + header_deps() + [__file__]):
         lang = ["-x", "hip"] if src.endswith(".hip") else []
-        run([HIPCC] + COMMON_FLAGS + list(extra) + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c"] + lang +
+        run([HIPCC] + COMMON_FLAGS + FILE_FLAGS.get(src, []) + list(extra) + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c"] + lang +
             [full, "-o", out])
     return out
 

@@ -44,8 +44,8 @@ def main():
         print(f"  {key}: {m.group(1) if m else '?'}")
     lines = [l.split("//")[0].strip() for l in f.splitlines()[1:]]
     addrs = [re.search(r"// ([0-9A-F]+):", l) for l in f.splitlines()[1:]]
-    # longest loop: a backward branch
-    best = (0, 0, 0)
+    # loops: backward branches
+    best, best_m = (0, 0, 0), -1
     for k, l in enumerate(f.splitlines()[1:]):
         m = re.search(r"s_cbranch_\w+ (\d+)|s_branch (\d+)", l)
         if m:
@@ -59,8 +59,10 @@ def main():
                     for j in range(k, -1, -1):
                         a = addrs[j]
                         if a and int(a.group(1), 16) - int(cands[0].split()[0], 16) <= t:
-                            if k - j > best[0]:
-                                best = (k - j, j, k)
+                            # the loop with the most MFMAs (then the longest) is the main loop
+                            nm = sum("mfma" in x for x in lines[j:k + 1])
+                            if (nm, k - j) > (best_m, best[0]):
+                                best, best_m = (k - j, j, k), nm
                             break
     body = [l for l in lines[best[1]:best[2] + 1] if l]
     marks = [k for k, l in enumerate(lines) if l.startswith("s_nop 15")]
