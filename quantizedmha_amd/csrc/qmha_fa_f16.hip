@@ -130,7 +130,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     v16f o[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) o[m] = v16f{};
-    float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290)
+    float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290); l_run per lane half
     unsigned long long stamp[4] = {0, 0, 0, 0};  // F16_STAMP diagnostics only
     const unsigned long long k_t0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long k_r0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -139,30 +139,36 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     const char* vbase = reinterpret_cast<const char*>(Vt + (size_t)bh * N * D);
     const int nst = (G + SG - 1) / SG;
 
+    // stages arrive by buffer_load ... lds: fixed per-lane source offsets, the stage offset in soffset
+    constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
+    int koff[KJ], voff[VJ];
+#pragma unroll
+    for (int jj = 0; jj < KJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ chunk_swz_h<RB>(row);
+        koff[jj] = row * RB + 16 * cc;
+    }
+#pragma unroll
+    for (int jj = 0; jj < VJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int grp = idx / (4 * D), w = idx % (4 * D);
+        const int d = w >> 2, cv = (w & 3) ^ chunk_swz_h<64>(d);
+        voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
+    }
     auto issue = [&](int buf, int st) {
         const int ngr = min(SG, G - st * SG);
-        const char* ksrc = kbase + (size_t)st * KBYTES;
-        const char* vsrc = vbase + (size_t)st * VBYTES;
         char* L = lds[buf];
 #pragma unroll
-        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+        for (int jj = 0; jj < KJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
-                const int idx = inst * 64 + lane;
-                const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ chunk_swz_h<RB>(row);
-                __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * RB + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
-            }
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
+                buffer_load_lds16(kbase, N * RB, (lptr_t)(L + inst * 1024), koff[jj], st * KBYTES);
         }
 #pragma unroll
-        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+        for (int jj = 0; jj < VJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
-                const int idx = inst * 64 + lane;
-                const int grp = idx / (4 * D), w = idx % (4 * D);
-                const int d = w >> 2, cv = (w & 3) ^ chunk_swz_h<64>(d);
-                __builtin_amdgcn_global_load_lds((gptr_t)(vsrc + grp * 64 * D + d * 64 + 16 * cv),
-                                                 (lptr_t)(L + KBYTES + inst * 1024), 16, 0, 0);
-            }
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
+                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
     // S^T = K Q^T (fp32 accumulate) of tile gi of the stage in LDS
@@ -178,10 +184,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     };
     // online softmax of one tile (fa_tc_v1a.cu:101-220) and O = alpha*O + P V (:207,:218)
     auto tile = [&](const char* L, int gi, const v16f& s) {
-        float mx = s[0];
+        float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);  // max3 chain
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
-        mx = half_swap_max(mx);
+        for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[r]), s[r + 1]);
+        mx = half_swap_max(fmaxf(mx, s[15]));
         const float m_new = fmaxf(m_run, mx * c_log2);
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         float p[16];
@@ -194,8 +200,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
             pop[r >> 3][r & 7] = h2[0];
             pop[r >> 3][(r & 7) + 1] = h2[1];
         }
-        const float rs = half_swap_add(tree_sum16(p));
-        l_run = fmaf(alpha, l_run, rs);  // :198
+        // this lane's half of the keys; the halves are joined once, in the epilogue
+        l_run = fmaf(alpha, l_run, tree_sum16(p));  // :198
         m_run = m_new;
         if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {  // exact skip when alpha == 1 for every row
 #pragma unroll
@@ -263,6 +269,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
                    __builtin_amdgcn_s_memtime() - k_t0, __builtin_amdgcn_s_memrealtime() - k_r0);
     }
     if (active) {
+        l_run = half_swap_add(l_run);
         const bool ok = l_run > 1e-10f;  // fa_tc_v1a.cu:384-388
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
