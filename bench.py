@@ -137,10 +137,28 @@ def cpu_baseline(budget_s=20.0):
         os.close(saved)
         os.close(devnull)
     value = flops(1, heads, N, d) / t / 1e12
-    return {"value": value, "unit": "TFLOPS", "cores": 1, "kind": kind,
-            "sample": f"utils/verify.cu cpu_reference (RoPE) B1 H{heads} N{N} d{d}, 1 thread, {t:.2f} s; "
-                      f"attention-equivalent 4*H*N^2*d FLOPs", "seconds": round(t, 3),
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
+    res = {"value": value, "unit": "TFLOPS", "cores": 1, "kind": kind,
+           "sample": f"utils/verify.cu cpu_reference (RoPE) B1 H{heads} N{N} d{d}, 1 thread, {t:.2f} s; "
+                     f"attention-equivalent 4*H*N^2*d FLOPs", "seconds": round(t, 3),
+           "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
+    res["port_int8"] = cpu_port_int8()
+    return res
+
+
+def cpu_port_int8(threads=16, N=4096, H=16, d=64):
+    """The same int8 algorithm as the GPU path (oracle/qmha_oracle.c oracle_fa_int8, the CPU
+    restatement of fa_tc_int8_b), multi-threaded over heads on `threads` host cores (the
+    GPU box's CPU share), on one sequence of the C4 shape: the practical CPU verify path."""
+    from oracle import oracle
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    rng = np.random.default_rng(7)
+    Q, K, V = (rng.standard_normal((N, H * d), dtype=np.float32) * 0.5 for _ in range(3))
+    t0 = time.perf_counter()
+    oracle.fa_int8(Q, K, V, H * d, H, nthreads=threads)
+    t = time.perf_counter() - t0
+    return {"value": flops(1, H, N, d) / t / 1e12, "unit": "TFLOPS", "cores": threads, "kind": "port",
+            "sample": f"oracle_fa_int8 B1 H{H} N{N} d{d} (one sequence of the C4 workload), "
+                      f"{threads} threads, {t:.2f} s", "seconds": round(t, 3)}
 
 
 def _cpu_model():
