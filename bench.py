@@ -87,6 +87,32 @@ def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=Tr
     }
 
 
+def time_solve_calls(variant, B, H, N, d, dev, reps=3):
+    """The reference's calling pattern (drivers/main.cu:135-142, torch_ext.cpp:36-40): one
+    blocking `solve` per sequence, B of them per step, through the C-ABI (qmha_solve_variant =
+    solve with the variant chosen at run time).  Returns ms per B calls."""
+    lib = _lib.load()
+    vid = _lib.variant_id(variant)
+    g = torch.Generator(device=dev).manual_seed(99)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    O = torch.empty_like(Q)
+    sz = N * H * d * 4
+
+    def calls():
+        for b in range(B):
+            st = lib.qmha_solve_variant(Q.data_ptr() + b * sz, K.data_ptr() + b * sz, V.data_ptr() + b * sz,
+                                        O.data_ptr() + b * sz, N, H * d, H, vid)
+            _lib.check(st, variant)
+
+    calls()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        calls()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) * 1e3 / reps
+
+
 def time_allgather(O, steps, dev, world):
     out = torch.empty((world,) + tuple(O.shape), dtype=O.dtype, device=dev)
     dist.all_gather_into_tensor(out, O)
@@ -262,6 +288,10 @@ def main():
                                              PEAKS[v], 4)}
             del rv
         res["siblings"] = sib
+    if rank == 0 and world == 1 and not a.no_siblings:
+        ms = time_solve_calls(a.variant, B, H, N, d, dev)
+        res["solve_calls"] = {"pattern": f"{B} blocking solve() calls, one per sequence (reference usage)",
+                              "ms_per_step": round(ms, 4), "tflops": round(flops(B, H, N, d) / (ms * 1e-3) / 1e12, 3)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline()
     if rank == 0:
