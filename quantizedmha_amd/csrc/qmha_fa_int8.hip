@@ -217,7 +217,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 // ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
 //   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8 };
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
 template <int D, int WAVES, int FL>
-__global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : 3) void qmha_fa_int8_pipe_kernel(
+__global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
@@ -840,7 +840,13 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
-    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
+#ifdef QMHA_ABLATION
+    // occupancy probe: unused dynamic LDS per workgroup caps the workgroups per CU
+    static const int lds_pad = std::getenv("QMHA_INT8_LDS_PAD") ? std::atoi(std::getenv("QMHA_INT8_LDS_PAD")) : 0;
+#else
+    constexpr int lds_pad = 0;
+#endif
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
                        w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
@@ -872,6 +878,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9040: return fa_int8_pipe_launch<D, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
+            case 9064: return fa_int8_pipe_launch<D, 4, FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
         // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
