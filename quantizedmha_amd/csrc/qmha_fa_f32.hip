@@ -261,6 +261,167 @@ __global__ __launch_bounds__(256) void qmha_fa_f32_v2_kernel(const float* __rest
     }
 }
 
+// v3: the v2 tiling generalised to RPT query rows per thread and NT threads (NT/8 * RPT rows per
+// workgroup).  RPT = 4 halves the LDS bytes per FMA of Q@K^T and P@V against v2's two rows (each
+// K / V / P vector read from LDS feeds RPT rows); the fmaf orders are v2's, so S is unchanged
+// bit for bit and O to the last ulp.
+template <int D, int RPT, int NT>
+__global__ __launch_bounds__(NT) void qmha_fa_f32_v3_kernel(const float* __restrict__ Q, const float* __restrict__ K,
+                                                             const float* __restrict__ V, float* __restrict__ O, int N,
+                                                             int H, int d_model, float inv_sqrt_d) {
+    constexpr int QS = D + 4;   // q row stride (floats): b128 row reads hit distinct banks
+    constexpr int KTS = 36;     // transposed K: [D][32 keys + 4]
+    constexpr int VS = D + 4;   // V rows
+    constexpr int PS = 36;      // P rows [R][32 + 4]
+    constexpr int CH = D / 32;  // 4-column output chunks per thread
+    constexpr int RS = NT / 8;            // row groups = row stride between a thread's rows
+    constexpr int R = RS * RPT;           // query rows per workgroup
+    constexpr int LD = 32 * D / 4 / NT;   // float4 of K (and of V) per thread per tile
+    static_assert(LD >= 1, "d >= 32");
+    __shared__ __attribute__((aligned(16))) float qs[R * QS];
+    __shared__ __attribute__((aligned(16))) float kt[D * KTS];
+    __shared__ __attribute__((aligned(16))) float vs[32 * VS];
+    __shared__ __attribute__((aligned(16))) float ps[R * PS];
+
+    const int G = N / QMHA_GROUP;
+    const int nqb = (N + R - 1) / R;  // R-row query blocks
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int tid = threadIdx.x, rp = tid >> 3, c = tid & 7;
+    const size_t head_off = (size_t)b * N * d_model + (size_t)k * D;
+    const int row0 = qb * R;
+
+    for (int i = tid; i < R * D / 4; i += NT) {
+        const int row = i / (D / 4), c4 = i % (D / 4);
+        v4f x = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (row0 + row < N) x = *reinterpret_cast<const v4f*>(Q + head_off + (size_t)(row0 + row) * d_model + 4 * c4);
+        *reinterpret_cast<v4f*>(&qs[row * QS + 4 * c4]) = x;
+    }
+    float o[RPT][CH][4];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+#pragma unroll
+        for (int h = 0; h < CH; ++h)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[i][h][e] = 0.0f;
+    float m_prev[RPT], l[RPT];  // m0 = 0 (fa.cu:279)
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) m_prev[i] = l[i] = 0.0f;
+
+    v4f kreg[LD], vreg[LD];
+    auto gload = [&](int t) {
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+            const int i = tid + NT * j, row = i / (D / 4), c4 = i % (D / 4);
+            const size_t g = head_off + (size_t)(t * 32 + row) * d_model + 4 * c4;
+            kreg[j] = *reinterpret_cast<const v4f*>(K + g);
+            vreg[j] = *reinterpret_cast<const v4f*>(V + g);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+            const int i = tid + NT * j, row = i / (D / 4), c4 = i % (D / 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) kt[(4 * c4 + e) * KTS + row] = kreg[j][e];
+            *reinterpret_cast<v4f*>(&vs[row * VS + 4 * c4]) = vreg[j];
+        }
+    };
+
+    gload(0);
+    for (int t = 0; t < G; ++t) {
+        __syncthreads();  // the previous tile's kt/vs/ps reads are done
+        lstore();
+        __syncthreads();
+        if (t + 1 < G) gload(t + 1);  // in flight during this tile's compute
+        // ---- S = Q K^T (fa.cu:24-102): sequential fmaf chain over k from 0, then * 1/sqrt(d)
+        float sacc[RPT][4] = {};
+#pragma unroll 4
+        for (int kk = 0; kk < D; kk += 4) {
+            v4f qv[RPT];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) qv[i] = *reinterpret_cast<const v4f*>(&qs[(rp + RS * i) * QS + kk]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const v4f kv = *reinterpret_cast<const v4f*>(&kt[(kk + e) * KTS + 4 * c]);
+#pragma unroll
+                for (int i = 0; i < RPT; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) sacc[i][j] = fmaf(qv[i][e], kv[j], sacc[i][j]);
+            }
+        }
+        // ---- online softmax per row (fa.cu:106-209); the row's 32 scores live on 8 lanes
+        float alpha[RPT];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            float mx = m_prev[i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sacc[i][j] *= inv_sqrt_d;  // fa.cu:141
+                mx = fmaxf(mx, sacc[i][j]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 1));
+            mx = fmaxf(mx, __shfl_xor(mx, 2));
+            mx = fmaxf(mx, __shfl_xor(mx, 4));
+            v4f pv;
+            float rs = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pv[j] = expf(sacc[i][j] - mx);  // fa.cu:167
+                rs += pv[j];
+            }
+            *reinterpret_cast<v4f*>(&ps[(rp + RS * i) * PS + 4 * c]) = pv;
+            rs += __shfl_xor(rs, 1);
+            rs += __shfl_xor(rs, 2);
+            rs += __shfl_xor(rs, 4);
+            alpha[i] = expf(m_prev[i] - mx);  // fa.cu:187
+            l[i] = fmaf(alpha[i], l[i], rs);  // fa.cu:190
+            m_prev[i] = mx;
+        }
+        __syncthreads();
+        // ---- O = alpha*O + P V (fa.cu:93-94,199): sequential fmaf chain over the tile's keys
+        float acc[RPT][CH][4] = {};
+#pragma unroll 2
+        for (int kv = 0; kv < 32; kv += 4) {
+            v4f pr[RPT];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) pr[i] = *reinterpret_cast<const v4f*>(&ps[(rp + RS * i) * PS + kv]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                for (int h = 0; h < CH; ++h) {
+                    const v4f vv = *reinterpret_cast<const v4f*>(&vs[(kv + e) * VS + 32 * h + 4 * c]);
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[i][h][j] = fmaf(pr[i][e], vv[j], acc[i][h][j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+#pragma unroll
+            for (int h = 0; h < CH; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[i][h][j] = __fadd_rn(__fmul_rn(o[i][h][j], alpha[i]), acc[i][h][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int row = row0 + rp + RS * i;
+        if (row >= N) continue;
+        const bool ok = l[i] > 1e-10f;  // fa.cu:371
+        float* orow = O + head_off + (size_t)row * d_model;
+#pragma unroll
+        for (int h = 0; h < CH; ++h) {
+            v4f w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = ok ? o[i][h][j] / l[i] : 0.0f;
+            *reinterpret_cast<v4f*>(orow + 32 * h + 4 * c) = w;
+        }
+    }
+}
+
 template <int D>
 static hipError_t fa_f32_v2(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream) {
@@ -268,6 +429,16 @@ static hipError_t fa_f32_v2(const float* Q, const float* K, const float* V, floa
     const float inv_sqrt_d = 1.0f / sqrtf((float)D);  // fa.cu:410
     hipLaunchKernelGGL((qmha_fa_f32_v2_kernel<D>), dim3(B * H * ((G + 1) / 2)), dim3(256), 0, stream, Q, K, V, O, N, H,
                        d_model, inv_sqrt_d);
+    return hipGetLastError();
+}
+
+template <int D, int RPT, int NT>
+static hipError_t fa_f32_v3(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
+                            hipStream_t stream) {
+    constexpr int R = NT / 8 * RPT;
+    const float inv_sqrt_d = 1.0f / sqrtf((float)D);  // fa.cu:410
+    hipLaunchKernelGGL((qmha_fa_f32_v3_kernel<D, RPT, NT>), dim3(B * H * ((N + R - 1) / R)), dim3(NT), 0, stream, Q, K,
+                       V, O, N, H, d_model, inv_sqrt_d);
     return hipGetLastError();
 }
 
@@ -283,7 +454,17 @@ static hipError_t fa_f32_d(const float* Q, const float* K, const float* V, float
 
 hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int D,
                          int d_model, hipStream_t stream) {
-    if (tune_config("QMHA_F32_CFG") != 1) {  // 1 = the v1 kernel
+    const int cfg = tune_config("QMHA_F32_CFG");
+    if (D == 64) {  // v3 tilings (rows per thread x threads); default 4 x 256 = 128 rows per workgroup
+        switch (cfg) {
+            case 34: return fa_f32_v3<64, 4, 128>(Q, K, V, O, B, N, H, d_model, stream);
+            case 36: return fa_f32_v3<64, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+            case 37: return fa_f32_v3<64, 2, 128>(Q, K, V, O, B, N, H, d_model, stream);
+            case 1: case 2: break;  // v1 / v2 below
+            default: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        }
+    }
+    if (cfg != 1) {  // 1 = the v1 kernel, 2 = v2
         switch (D) {
             case 32: return fa_f32_v2<32>(Q, K, V, O, B, N, H, d_model, stream);
             case 64: return fa_f32_v2<64>(Q, K, V, O, B, N, H, d_model, stream);
