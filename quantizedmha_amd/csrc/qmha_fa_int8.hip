@@ -548,9 +548,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
     }
-    auto issue = [&](int st) {
+    // stage st into ring slot `slot` (= st % RING; a compile-time constant in the unrolled loop)
+    auto issue_at = [&](int st, int slot) {
         const int ngr = min(SG, G - st * SG);
-        int8_t* L = lds[st % RING];
+        int8_t* L = lds[slot];
 #pragma unroll
         for (int jj = 0; jj < KJ; ++jj) {
             const int inst = wave + jj * WAVES;
@@ -564,18 +565,21 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
-    // operand reads of tile t from the ring
-    auto kop_of = [&](int t, int ks) {
-        const int8_t* L = lds[(t >> 1) % RING];
-        const int krow = (t & 1) * 32 + col;
+    auto issue = [&](int st) { issue_at(st, st % RING); };
+    // operand reads of the tile in ring slot `slot`, position `par` (0/1) of its stage
+    auto kop_at = [&](int slot, int par, int ks) {
+        const int8_t* L = lds[slot];
+        const int krow = par * 32 + col;
         return *reinterpret_cast<const v4i*>(L + krow * D + 16 * ((2 * ks + half) ^ chunk_swz<D>(krow)));
     };
-    auto vop_of = [&](int t, int m, int ks) {
-        const int8_t* L = lds[(t >> 1) % RING];
+    auto vop_at = [&](int slot, int par, int m, int ks) {
+        const int8_t* L = lds[slot];
         const int d = 32 * m + col;
-        return *reinterpret_cast<const v8h*>(L + KBYTES + (t & 1) * 64 * D + d * 64 +
+        return *reinterpret_cast<const v8h*>(L + KBYTES + par * 64 * D + d * 64 +
                                              16 * ((2 * ks + half) ^ chunk_swz<64>(d)));
     };
+    auto kop_of = [&](int t, int ks) { return kop_at((t >> 1) % RING, t & 1, ks); };
+    auto vop_of = [&](int t, int m, int ks) { return vop_at((t >> 1) % RING, t & 1, m, ks); };
 
     v16i magic_blk;
 #pragma unroll
@@ -598,12 +602,24 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 1), qop[1], s_cur, 0, 0, 0);
 
 #define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
-    // one pipeline iteration; HP / HN (compile time): a tile t-1 to finish / a tile t+1 to start
-    auto iter = [&](int t, auto HP, auto HN) {
+    // one pipeline iteration; HP / HN (compile time): a tile t-1 to finish / a tile t+1 to start.
+    // PH (compile time): -1, or u with t = 6j + 1 + u, which fixes every ring slot and stage
+    // position this iteration touches (the ring has 3 slots of 2 tiles: period 6), so operand
+    // reads are LDS immediates and the per-tile slot arithmetic disappears
+    auto iter = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
-        if (t & 1) {  // uniform
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_n = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        auto vop_of = [&](int, int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto kop_of = [&](int, int ks) { return kop_at(slot_n, par_n, ks); };            // tile t+1
+        if (odd) {  // uniform
             qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
-            if ((t >> 1) + 2 < nst) issue((t >> 1) + 2);
+            if ((t >> 1) + 2 < nst)
+                issue_at((t >> 1) + 2, ph >= 0 ? ((((1 + ph) >> 1) + 2) % RING) : (((t >> 1) + 2) % RING));
         }
         // operand reads for this iteration's MFMAs
         v8h v00, v01, v10, v11;
@@ -718,9 +734,19 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
     // G >= 2 (the launcher routes N < 64 elsewhere): first, interior, last tile
-    iter(0, F0{}, T1{});
-    for (int t = 1; t < G - 1; ++t) iter(t, T1{}, T1{});
-    iter(G - 1, T1{}, F0{});
+    using DYN = std::integral_constant<int, -1>;
+    iter(0, F0{}, T1{}, DYN{});
+    int t = 1;
+    for (; t + 6 <= G - 1; t += 6) {
+        iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
+        iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
+        iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
+        iter(t + 3, T1{}, T1{}, std::integral_constant<int, 3>{});
+        iter(t + 4, T1{}, T1{}, std::integral_constant<int, 4>{});
+        iter(t + 5, T1{}, T1{}, std::integral_constant<int, 5>{});
+    }
+    for (; t < G - 1; ++t) iter(t, T1{}, T1{}, DYN{});
+    iter(G - 1, T1{}, F0{}, DYN{});
 #undef QMHA_FENCE
     // drain: P@V of the last tile
     {
