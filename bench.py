@@ -223,6 +223,9 @@ def main():
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--no-siblings", action="store_true", help="skip the fp16 / fp32 sibling measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-solve-calls", action="store_true",
+                    help="skip the one-solve-per-sequence timing (profiled runs: keeps its B=1 launches "
+                         "out of the main kernel's rocprof average)")
     ap.add_argument("--allgather", action="store_true", default=None,
                     help="time the RCCL all-gather of per-shard outputs (default on when N>1)")
     a = ap.parse_args()
@@ -288,7 +291,7 @@ def main():
                                              PEAKS[v], 4)}
             del rv
         res["siblings"] = sib
-    if rank == 0 and world == 1 and not a.no_siblings:
+    if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls:
         ms = time_solve_calls(a.variant, B, H, N, d, dev)
         res["solve_calls"] = {"pattern": f"{B} blocking solve() calls, one per sequence (reference usage)",
                               "ms_per_step": round(ms, 4), "tflops": round(flops(B, H, N, d) / (ms * 1e-3) / 1e12, 3)}

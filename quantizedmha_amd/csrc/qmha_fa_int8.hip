@@ -214,10 +214,15 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //               subtract recovers float(S) for two scores (replaces two v_cvt_f32_i32)
 //   FL_PREFETCH Q@K^T of tile t+1 issued before the softmax of tile t (QPW == 1)
 //   FL_LB2      register budget of 2 waves per SIMD (256 VGPRs) instead of 4 (128)
+//   FL_JIT / FL_LB4 (pipe kernel) operands read right before their MFMA / 4-wave register budget
+//   FL_EARLY    (pipe kernel) a tile's serial head (row max .. 1/sP) computed in the previous
+//               iteration beside its O update
+//   FL_KFOLD    (pipe kernel, with FL_MAGIC) the exponent read straight off the biased
+//               accumulator: the bias folded into the shift (see the kernel)
 // ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
 //   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16 };
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -594,12 +599,50 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
     float scale_cur = 0.0f, scale_prev = 0.0f;
     v16f a0, a1;                 // P@V accumulators of the pending tile
+    constexpr bool EARLY = FL & FL_EARLY;
+    // FL_KFOLD (with FL_MAGIC): the exponent of key j is fma(A_j, c', -Kn) straight from the
+    // biased accumulator A_j = 1.5*2^23 + S_j (as a float), with Kn = 1.5*2^23*c' + m.  c' is the
+    // score scale rounded to 22 significant bits, so 1.5*2^23*c' is exact and the shift the
+    // exponents actually get, m_eff = Kn - 1.5*2^23*c', is exact too (Sterbenz: |m| < 2^20 c').
+    // So p'_j = 2^(s_j - m_eff) = p_j * 2^(m_eff - m) with |m_eff - m| <= ulp(Kn)/2 (~1e-4): the
+    // per-row factor f = 2^(m_eff - m) (= 1 + (m_eff - m) ln 2 to < 1 ulp) is folded into the
+    // row's 1/sP and its row-sum scale, because the P tile's one scale sP is shared by rows with
+    // different f.  Saves the 16 bias subtractions per tile for 4 per-row operations.
+    constexpr bool KFOLD = MAGIC && (FL & FL_KFOLD);
+    // FL_EARLY: the serial head of a tile (row max -> running max -> P-tile max -> sP -> 1/sP)
+    // runs at the end of the previous iteration, in one scheduling region with that
+    // iteration's O update, so its latency chain interleaves with independent work
+    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f;
+    auto head = [&](const v16i& s, int t) {
+        float c = cq * skb[t];
+        const int mxi = half_swap_max_i(tree_max16_i(s));
+        float xmax;
+        if constexpr (KFOLD) {
+            c = __int_as_float((__float_as_int(c) + 2) & ~3);
+            const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;  // exact float(S_max)
+            h_m = fmaxf(m_run, sfmax * c);
+            h_k = fmaf(c, QMHA_MAGIC_RNE, h_m);
+            const float delta = fmaf(c, -QMHA_MAGIC_RNE, h_k) - h_m;  // m_eff - m, exact
+            h_f = fmaf(delta, 0.69314718055994531f, 1.0f);
+            xmax = fmaf(sfmax, c, -h_m);
+        } else {
+            const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
+            h_m = fmaxf(m_run, mx * c);
+            xmax = fmaf(mx, c, -h_m);
+        }
+        h_c = c;
+        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
+        h_sp = fmaxf(div127_fast(pmax), 1e-8f);
+        h_invp = rcp_fast(h_sp);
+        if constexpr (KFOLD) h_invp *= h_f;
+    };
 
     issue(0);
     if (nst > 1) issue(1);
     qmha_dma_barrier();
     s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 0), qop[0], magic_blk, 0, 0, 0);
     s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 1), qop[1], s_cur, 0, 0, 0);
+    if constexpr (EARLY) head(s_cur, 0);
 
 #define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
     // one pipeline iteration; HP / HN (compile time): a tile t-1 to finish / a tile t+1 to start.
@@ -637,23 +680,25 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         }
         QMHA_FENCE();
         // ---- A: row max, running max, P-tile max (fa_tc_int8_b.cu:286-303, :359)
-        const float c = cq * skb[t];
-        const int mxi = half_swap_max_i(tree_max16_i(s_cur));
-        const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
-        const float m_new = fmaxf(m_run, mx * c);
-        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
-        QMHA_FENCE();
+        if constexpr (!EARLY) {
+            head(s_cur, t);
+            QMHA_FENCE();
+        }
+        const float c = h_c, m_new = h_m, kn = h_k;
         if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0);
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
-        const float sp = fmaxf(div127_fast(pmax), 1e-8f);
-        const float invp = rcp_fast(sp);
+        const float sp = h_sp, invp = h_invp;
         const float e = __builtin_amdgcn_exp2f(m_new - anchor);
         float x[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
-            x[r] = fmaf(sv, c, -m_new);
+            if constexpr (KFOLD) {
+                x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+            } else {
+                const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+                x[r] = fmaf(sv, c, -m_new);
+            }
         }
         QMHA_FENCE();
         if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 0) : v10, pp0, v16f{}, 0, 0, 0);
@@ -661,8 +706,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- C: scores of rows 8..15
 #pragma unroll
         for (int r = 8; r < 16; ++r) {
-            const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
-            x[r] = fmaf(sv, c, -m_new);
+            if constexpr (KFOLD) {
+                x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+            } else {
+                const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+                x[r] = fmaf(sv, c, -m_new);
+            }
         }
         QMHA_FENCE();
         if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 1) : v01, pp1, a0, 0, 0, 0);
@@ -703,7 +752,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
         const float rs = tree_sum16(p);
-        l_run = fmaf(rs, e, l_run);
+        l_run = fmaf(rs, KFOLD ? e * h_f : e, l_run);
         m_run = m_new;
         const float scale_t = sp * svb[t] * e * 16777216.0f;  // 2^24: P entries are Pi * 2^-24
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
@@ -713,6 +762,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
             for (int r = 0; r < 16; ++r) o1[r] = fmaf(a1[r], scale_prev, o1[r]);
         }
+        if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
         QMHA_FENCE();
         scale_cur = scale_t;
         // re-anchor (rare): keep 2^(m - anchor) far from fp32 overflow; the tile whose P@V is
@@ -905,10 +955,15 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             case 9064: return fa_int8_pipe_launch<D, 4, FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9044: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
+            case 9049: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY | FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
+            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
+            case 9043: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
-        // default at d = 64: the software-pipelined kernel (1-2 % ahead of the others, r01 A/B)
-        return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
+        // default at d = 64: the software-pipelined kernel with the folded score bias
+        // (KFOLD: -2 % against plain MAGIC on one box, profiles/r01/overlap_sweep.txt)
+        return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
     }
     return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
 }

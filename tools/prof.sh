@@ -14,7 +14,7 @@ rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json | head -c 1500; echo
 if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi
 # the same bench command under the profiler (its JSON line lands in trace.log: its hipEvent
 # main_kernel_ms and rocprof's average for the main kernel describe the same launches)
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-solve-calls > $OUT/trace.log 2>&1
 rc=$?; echo "rocprof trace rc=$rc"
 if [ $rc -ne 0 ]; then tail -20 $OUT/trace.log; exit $rc; fi
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
