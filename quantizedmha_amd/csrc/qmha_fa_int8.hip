@@ -497,7 +497,7 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
-template <int D, int WAVES, int FL>
+template <int D, int WAVES, int FL, int PAD = 0>
 __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
@@ -596,6 +596,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
+    auto qk0 = [&](const v4i& k, const v4i& q) {
+        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, magic_blk, 0, 0, 0);
+    };
+    auto qk1 = [&](const v4i& k, const v4i& q) {
+        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, s_nxt, 0, 0, 0);
+    };
     v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
     float scale_cur = 0.0f, scale_prev = 0.0f;
     v16f a0, a1;                 // P@V accumulators of the pending tile
@@ -640,8 +646,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     issue(0);
     if (nst > 1) issue(1);
     qmha_dma_barrier();
-    s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 0), qop[0], magic_blk, 0, 0, 0);
-    s_cur = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop_of(0, 1), qop[1], s_cur, 0, 0, 0);
+    qk0(kop_of(0, 0), qop[0]);
+    qk1(kop_of(0, 1), qop[1]);
+    s_cur = s_nxt;
     if constexpr (EARLY) head(s_cur, 0);
 
 #define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -685,7 +692,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             QMHA_FENCE();
         }
         const float c = h_c, m_new = h_m, kn = h_k;
-        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0);
+        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a0) : "v"(pp0), "v"(pp1)); else a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0); }
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         QMHA_FENCE();
-        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 0) : v10, pp0, v16f{}, 0, 0, 0);
+        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a1) : "v"(pp0), "v"(pp1)); else a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 0) : v10, pp0, v16f{}, 0, 0, 0); }
         QMHA_FENCE();
         // ---- C: scores of rows 8..15
 #pragma unroll
@@ -714,20 +721,20 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         QMHA_FENCE();
-        if constexpr (has_prev) a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 1) : v01, pp1, a0, 0, 0, 0);
+        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a0) : "v"(pp0), "v"(pp1)); else a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 1) : v01, pp1, a0, 0, 0, 0); }
         QMHA_FENCE();
         // ---- D: p = exp2, rows 0..7
         float p[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(JIT ? kop_of(t + 1, 0) : k0, qop[0], magic_blk, 0, 0, 0);
+        if constexpr (has_next) { if constexpr (PAD >= 20000) asm volatile("" : "=v"(s_nxt) : "v"(qop[0]), "v"(magic_blk)); else qk0(JIT ? kop_of(t + 1, 0) : k0, qop[0]); }
         QMHA_FENCE();
         // ---- E: p = exp2, rows 8..15
 #pragma unroll
         for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_prev) a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 1) : v11, pp1, a1, 0, 0, 0);
+        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a1) : "v"(pp0), "v"(pp1)); else a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 1) : v11, pp1, a1, 0, 0, 0); }
         QMHA_FENCE();
         // ---- F: Pi = rint(p/sP) (:317-321), carried as the f16 subnormal Pi * 2^-24:
         // fma(p, 1/sP, 1.5 * 2^23) rounds half-even to an integer whose float bits end in Pi,
@@ -747,8 +754,26 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         QMHA_FENCE();
-        if constexpr (has_next) s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(JIT ? kop_of(t + 1, 1) : k1, qop[1], s_nxt, 0, 0, 0);
+        if constexpr (has_next) { if constexpr (PAD >= 20000) asm volatile("" : "=v"(s_nxt) : "v"(qop[0]), "v"(magic_blk)); else qk1(JIT ? kop_of(t + 1, 1) : k1, qop[1]); }
         QMHA_FENCE();
+#ifdef QMHA_ABLATION
+        // perturbation (timing only): PAD % 100 extra independent v_add_f32 and (PAD % 10000) / 100 extra
+        // v_exp_f32 per tile on two dead registers (PAD >= 10000: MFMAs replaced, see below), to measure the marginal issue cost
+        if constexpr (PAD > 0) {
+            float z0 = __builtin_bit_cast(float, lane), z1 = z0;
+#pragma unroll
+            for (int i = 0; i < PAD % 100; ++i) {
+                if (i & 1) asm volatile("v_add_f32 %0, %0, %0" : "+v"(z1));
+                else asm volatile("v_add_f32 %0, %0, %0" : "+v"(z0));
+            }
+#pragma unroll
+            for (int i = 0; i < (PAD % 10000) / 100; ++i) {
+                if (i & 1) asm volatile("v_exp_f32 %0, %0" : "+v"(z1));
+                else asm volatile("v_exp_f32 %0, %0" : "+v"(z0));
+            }
+            asm volatile("" ::"v"(z0), "v"(z1));
+        }
+#endif
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
         const float rs = tree_sum16(p);
@@ -779,7 +804,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         pp0 = pc0;
         pp1 = pc1;
         scale_prev = scale_cur;
-        s_cur = s_nxt;
+        if constexpr (has_next) s_cur = s_nxt;
     };
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
@@ -909,7 +934,7 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
     return hipGetLastError();
 }
 
-template <int D, int WAVES, int FL>
+template <int D, int WAVES, int FL, int PAD = 0>
 static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
                                       int d_model, hipStream_t stream) {
     const int G = N / QMHA_GROUP;
@@ -922,7 +947,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
 #else
     constexpr int lds_pad = 0;
 #endif
-    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
                        w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
@@ -943,6 +968,14 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, Qf, O, B, N, H, d_model, stream);
             case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, Qf, O, B, N, H, d_model, stream);
             case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, Qf, O, B, N, H, d_model, stream);
+            case 1008: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 8>(w, Qf, O, B, N, H, d_model, stream);
+            case 1016: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 16>(w, Qf, O, B, N, H, d_model, stream);
+            case 1032: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 32>(w, Qf, O, B, N, H, d_model, stream);
+            case 1400: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 400>(w, Qf, O, B, N, H, d_model, stream);
+            case 1800: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 800>(w, Qf, O, B, N, H, d_model, stream);
+            case 11000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 10000>(w, Qf, O, B, N, H, d_model, stream);
+            case 12000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 20000>(w, Qf, O, B, N, H, d_model, stream);
+            case 13000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 30000>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
