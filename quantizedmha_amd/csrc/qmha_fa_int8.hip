@@ -222,7 +222,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 // ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
 //   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64 };
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64, FL_AQK = 128 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -596,11 +596,35 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
+    // FL_AQK: Q@K^T accumulates in AGPRs (inline-asm MFMAs on s_acc, bias block in AGPRs) and S^T
+    // is read back by 16 v_accvgpr_read at the end of the iteration: a VGPR-form MFMA is
+    // serialised with VALU issue (profiles/r01/perturbation_int8.txt), an AGPR-form one is not.
+    // Needs the AGPR budget set in the IR ("amdgpu-agpr-alloc"), see tools/build.py.
+    constexpr bool AQK = FL & FL_AQK;
+    v16i s_acc, magic_a;
+    if constexpr (AQK) {
+        magic_a = magic_blk;
+        asm volatile("" : "+a"(magic_a));
+    }
     auto qk0 = [&](const v4i& k, const v4i& q) {
-        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, magic_blk, 0, 0, 0);
+        if constexpr (AQK)
+            asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %3" : "=&a"(s_acc) : "v"(k), "v"(q), "a"(magic_a));
+        else
+            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, magic_blk, 0, 0, 0);
     };
     auto qk1 = [&](const v4i& k, const v4i& q) {
-        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, s_nxt, 0, 0, 0);
+        if constexpr (AQK)
+            asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(s_acc) : "v"(k), "v"(q));
+        else
+            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, s_nxt, 0, 0, 0);
+    };
+    // S^T of the tile in flight into VGPRs (AQK); placed >= 50 instructions after its last MFMA
+    // (the 16-pass MFMA needs 18 wait states before a v_accvgpr_read of its result)
+    auto read_s = [&]() {
+        v16i r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[i]) : "a"(s_acc[i]));
+        return r;
     };
     v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
     float scale_cur = 0.0f, scale_prev = 0.0f;
@@ -648,7 +672,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     qmha_dma_barrier();
     qk0(kop_of(0, 0), qop[0]);
     qk1(kop_of(0, 1), qop[1]);
-    s_cur = s_nxt;
+    if constexpr (AQK) {
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> v_accvgpr_read
+        s_cur = read_s();
+    } else {
+        s_cur = s_nxt;
+    }
     if constexpr (EARLY) head(s_cur, 0);
 
 #define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -804,7 +833,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         pp0 = pc0;
         pp1 = pc1;
         scale_prev = scale_cur;
-        if constexpr (has_next) s_cur = s_nxt;
+        if constexpr (has_next) {
+            if constexpr (AQK) s_cur = read_s();
+            else s_cur = s_nxt;
+        }
     };
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
@@ -992,6 +1024,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9049: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY | FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
             case 9043: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
+            case 9045: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_AQK>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
         // default at d = 64: the software-pipelined kernel with the folded score bias
