@@ -87,12 +87,6 @@ def build(jobs=8, verbose=True):
                                      (f"-DQMHA_SOLVE_VARIANT={vid}", f"-DQMHA_SOLVE_NAME={name}"))
                      for name, vid in VARIANTS.items()}
         drv_objs = list(ex.map(compile_one, DRIVER_SOURCES))
-        co_srcs = list(ex.map(agpr_module, AGPR_MODULES))
-    for c in co_srcs:
-        out = c.replace(".cpp", ".o")
-        if newer(out, [c]):
-            run([HIPCC, "-O1", "-fPIC", "-c", c, "-o", out])
-        objs.append(out)
         shim_objs = {k: v.result() for k, v in shim_objs.items()}
     libqmha = os.path.join(LIB, "libqmha.so")
     if newer(libqmha, objs):
