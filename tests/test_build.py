@@ -1,0 +1,36 @@
+"""CPU test: HEAD builds from a clean tree.
+
+`__graft_entry__.build()` runs in a temporary copy of the source tree with no build/,
+no lib/ and no bin/, so a broken build script can never again ship binaries the sources
+cannot reproduce (round-1 VERDICT, "HEAD does not build").  The copy is sources only;
+/root/reference is read in place by oracle/Makefile when it exists.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SKIP_DIRS = {".git", "build", "lib", "bin", "alt_lib", "gpurun_out", "_ref", "__pycache__", ".pytest_cache",
+             "profiles", "golden"}
+
+
+def _ignore(_dir, names):
+    return [n for n in names if n in SKIP_DIRS or n.endswith((".so", ".o", ".pyc"))]
+
+
+@pytest.mark.timeout(600)
+def test_graft_entry_build_from_clean_copy(tmp_path):
+    dst = tmp_path / "repo"
+    shutil.copytree(ROOT, dst, ignore=_ignore)
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.build()"], cwd=dst,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    lib = dst / "quantizedmha_amd" / "lib"
+    for name in ("libqmha.so", "libqmha_fa.so", "libqmha_fa_tc_v1a.so", "libqmha_fa_tc_int8_b.so",
+                 "libqmha_unfused.so"):
+        assert (lib / name).is_file(), name
+    assert (dst / "quantizedmha_amd" / "bin" / "qmha_profile").is_file()
+    assert (dst / "oracle" / "liboracle.so").is_file()
