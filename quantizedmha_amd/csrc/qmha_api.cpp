@@ -112,8 +112,12 @@ std::atomic<int> g_overlap_chunks{-1};  // -1: not yet read from QMHA_OVERLAP_CH
 int overlap_chunks(int B) {
     int c = g_overlap_chunks.load();
     if (c < 0) {
+#ifdef QMHA_ABLATION  // profiling builds: QMHA_OVERLAP_CHUNKS sets the default (production: the API only)
         const char* e = std::getenv("QMHA_OVERLAP_CHUNKS");
         c = e ? std::atoi(e) : 1;
+#else
+        c = 1;
+#endif
         c = c < 1 ? 1 : (c > 16 ? 16 : c);
         g_overlap_chunks.store(c);
     }

@@ -332,6 +332,7 @@ static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float
 template <int D>
 static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                            hipStream_t stream) {
+#ifdef QMHA_ABLATION  // tuning alternatives: profiling builds only
     if constexpr (D == 64) {
         switch (tune_config("QMHA_F16_CFG")) {
             case 420: return fa_f16_v2_launch<D, 4, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
@@ -340,13 +341,12 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
             case 441: return fa_f16_v2_launch<D, 4, 4, F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 424: return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
             case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
-#ifdef QMHA_ABLATION
             case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
             case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, Qf, O, B, N, H, d_model, stream);
-#endif
             default: break;
         }
     }
+#endif
     // default: v2 (LDS-DMA staging, per-tile softmax), 4 waves/SIMD budget (r01 A/B: 1.54 ms vs
     // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64)
     return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);

@@ -454,28 +454,24 @@ static hipError_t fa_f32_d(const float* Q, const float* K, const float* V, float
 
 hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int D,
                          int d_model, hipStream_t stream) {
+#ifdef QMHA_ABLATION  // tuning alternatives and the v1/v2 kernels at d = 64: profiling builds only
     const int cfg = tune_config("QMHA_F32_CFG");
-    if (D == 64) {  // v3 tilings (rows per thread x threads); default 4 x 256 = 128 rows per workgroup
+    if (D == 64) {
         switch (cfg) {
             case 34: return fa_f32_v3<64, 4, 128>(Q, K, V, O, B, N, H, d_model, stream);
             case 36: return fa_f32_v3<64, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
             case 37: return fa_f32_v3<64, 2, 128>(Q, K, V, O, B, N, H, d_model, stream);
-            case 1: case 2: break;  // v1 / v2 below
-            default: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
+            case 1: return fa_f32_d<64>(Q, K, V, O, B, N, H, d_model, stream);
+            case 2: return fa_f32_v2<64>(Q, K, V, O, B, N, H, d_model, stream);
+            default: break;
         }
     }
-    if (cfg != 1) {  // 1 = the v1 kernel, 2 = v2
-        switch (D) {
-            case 32: return fa_f32_v2<32>(Q, K, V, O, B, N, H, d_model, stream);
-            case 64: return fa_f32_v2<64>(Q, K, V, O, B, N, H, d_model, stream);
-            case 128: return fa_f32_v2<128>(Q, K, V, O, B, N, H, d_model, stream);
-            default: return hipErrorInvalidValue;
-        }
-    }
+#endif
+    // d = 64: v3 (4 rows x 4 keys per thread, 256 threads = 128 rows per workgroup); else v2
     switch (D) {
-        case 32: return fa_f32_d<32>(Q, K, V, O, B, N, H, d_model, stream);
-        case 64: return fa_f32_d<64>(Q, K, V, O, B, N, H, d_model, stream);
-        case 128: return fa_f32_d<128>(Q, K, V, O, B, N, H, d_model, stream);
+        case 32: return fa_f32_v2<32>(Q, K, V, O, B, N, H, d_model, stream);
+        case 64: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 128: return fa_f32_v2<128>(Q, K, V, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -374,6 +374,17 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
             // reference's O = alpha*O + T*sP*sV and l = alpha*l + rowsum (:336,:344,:369-371)
             // become o += T*sP*sV*2^(m_t - anchor) and l_run += rowsum*2^(m_t - anchor):
             // mathematically identical, no per-tile pass over O and no alpha.
+            // re-anchor before the shift is formed, so 2^(m_new - anchor) <= 2^48 whatever the jump
+            // of the running max (a first tile ~100 log2 units above m0 = 0 would overflow it)
+            if (__builtin_amdgcn_ballot_w64(m_new - anchor[j] > 48.0f)) {
+                const float f = __builtin_amdgcn_exp2f(anchor[j] - m_new);
+#pragma unroll
+                for (int m = 0; m < KS; ++m)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[j][m][r] *= f;
+                l_run[j] *= f;
+                anchor[j] = m_new;
+            }
             const float e = __builtin_amdgcn_exp2f(m_new - anchor[j]);
             l_run[j] = fmaf(rs, e, l_run[j]);
             m_run[j] = m_new;
@@ -446,19 +457,6 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
                     v16i s[QPW];
                     qk(L, gi, s);
                     tile(L, gi, g0 + gi, s);
-                }
-            }
-            // re-anchor (rare, once per stage): keep 2^(m - anchor) far from fp32 overflow
-#pragma unroll
-            for (int j = 0; j < QPW; ++j) {
-                if (__builtin_amdgcn_ballot_w64(m_run[j] - anchor[j] > 48.0f)) {
-                    const float f = __builtin_amdgcn_exp2f(anchor[j] - m_run[j]);
-#pragma unroll
-                    for (int m = 0; m < KS; ++m)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) o[j][m][r] *= f;
-                    l_run[j] *= f;
-                    anchor[j] = m_run[j];
                 }
             }
         }
@@ -721,6 +719,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             QMHA_FENCE();
         }
         const float c = h_c, m_new = h_m, kn = h_k;
+        // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
+        // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
+        // overflow it); the pending tile t-1 carries its factor in scale_prev
+        if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+            const float f = __builtin_amdgcn_exp2f(anchor - m_new);
+            o0 *= f;
+            o1 *= f;
+            l_run *= f;
+            scale_prev *= f;
+            anchor = m_new;
+        }
         if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a0) : "v"(pp0), "v"(pp1)); else a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0); }
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
@@ -819,16 +828,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
         QMHA_FENCE();
         scale_cur = scale_t;
-        // re-anchor (rare): keep 2^(m - anchor) far from fp32 overflow; the tile whose P@V is
-        // still pending carries its factor in scale_cur
-        if (__builtin_amdgcn_ballot_w64(m_run - anchor > 48.0f)) {
-            const float f = __builtin_amdgcn_exp2f(anchor - m_run);
-            o0 *= f;
-            o1 *= f;
-            l_run *= f;
-            scale_cur *= f;
-            anchor = m_run;
-        }
         // rotate the pipeline
         pp0 = pc0;
         pp1 = pc1;
@@ -984,7 +983,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     return hipGetLastError();
 }
 
-// Default geometry per head size, and the QMHA_INT8_CFG tuning alternatives (profiling).
+// Default geometry per head size (QMHA_INT8_CFG tuning alternatives: QMHA_ABLATION builds only).
 template <int D>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream) {
@@ -1010,7 +1009,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 13000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 30000>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
-#endif
+        // tuning alternatives (profiling builds only: the production library has one kernel per d)
         switch (tune_config("QMHA_INT8_CFG")) {
             case 4120: return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
             case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
@@ -1027,6 +1026,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9045: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_AQK>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
+#endif
         // default at d = 64: the software-pipelined kernel with the folded score bias
         // (KFOLD: -2 % against plain MAGIC on one box, profiles/r01/overlap_sweep.txt)
         return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);

@@ -135,3 +135,24 @@ def test_slot_permutations_are_bijective():
                 assert kv_f16[16 * s + 8 * h + e] == acc_row(8 * s + e, h)
     assert np.array_equal(np.argsort(kv_f16), [16 * (kv >> 4) + 8 * ((kv >> 2) & 1) + (kv & 3) + 4 * ((kv >> 3) & 1)
                                                for kv in range(32)])
+
+
+def test_production_library_has_one_kernel_per_variant_and_d(built):
+    """No tuning/ablation alternates in the shipped libqmha.so (round-1 ADVICE): every kernel
+    template is instantiated at most once per head size, and no QMHA_*_CFG / overlap
+    environment switch exists (those live in QMHA_ABLATION builds only)."""
+    path = os.path.join(LIB_DIR, "libqmha.so")
+    syms = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
+    stubs = set(re.findall(r"__device_stub__(\w+?)ILi(\d+)E(\w*)", syms))
+    per = {}
+    for name, d, rest in stubs:
+        if name.startswith("qmha_gemm"):
+            continue
+        per.setdefault((name, d), set()).add(rest)
+    assert per, syms[:2000]
+    for (name, d), inst in per.items():
+        limit = 2 if name == "qmha_quant_int8_kernel" else 1  # the V layout is a template argument
+        assert len(inst) <= limit, (name, d, sorted(inst))
+    blob = open(path, "rb").read()
+    for env in (b"QMHA_INT8_CFG", b"QMHA_F16_CFG", b"QMHA_F32_CFG", b"QMHA_OVERLAP_CHUNKS", b"QMHA_INT8_ABL"):
+        assert env not in blob, env

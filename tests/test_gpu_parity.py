@@ -182,6 +182,37 @@ def test_growing_scores_reanchor(dev, oracle_mod, variant):
     assert_parity(variant, out, ref, scale=5.0 if variant == "fa_tc_v1a" else 1.0)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_large_first_tile_and_spike_no_overflow(dev, oracle_mod, variant, d):
+    """Running-max jumps far beyond the int8 kernel's 48-log2 anchor headroom in ONE tile.
+
+    (1) constant Q = K = 3.5: every score is 3.5^2 * sqrt(d) (98 nats at d = 64, ~141 log2
+    units above m0 = 0) already in the first tile; the reference returns mean(V) per head.
+    (2) a single key tile whose scores sit ~200 log2 units above the rest mid-sequence.
+    Before the fix the shift 2^(m_new - anchor) overflowed to inf, the re-anchor made it NaN
+    and the epilogue's l > 1e-20 guard silently wrote 0 (round-1 ADVICE, qmha_fa_int8.hip:728)."""
+    N, h = 256, 2
+    dm = d * h
+    rng = np.random.default_rng(40 + d)
+    Q = np.full((N, dm), 3.5, np.float32)
+    K = np.full((N, dm), 3.5, np.float32)
+    V = rng.standard_normal((N, dm)).astype(np.float32)
+    out = run(variant, Q, K, V, dm, h, dev)
+    ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
+    assert np.isfinite(out).all()
+    assert np.abs(ref - V.mean(axis=0, keepdims=True)).max() <= 5e-2  # the oracle really averages V
+    assert_parity(variant, out, ref)
+    # spike: keys 160..191 (one 32-key tile) strongly aligned with every query
+    Q = (rng.standard_normal((N, dm)) * 0.3 + 1.0).astype(np.float32)
+    K = (rng.standard_normal((N, dm)) * 0.3).astype(np.float32)
+    K[160:192] = 6.0
+    out = run(variant, Q, K, V, dm, h, dev)
+    ref = oracle_for(oracle_mod, variant)(Q, K, V, dm, h)
+    assert np.isfinite(out).all() and np.abs(out).max() > 0.01
+    assert_parity(variant, out, ref, scale=5.0 if variant == "fa_tc_v1a" else 1.0)
+
+
 @pytest.mark.parametrize("variant", ["fa_tc_int8_b", "fa_tc_v1a", "fa"])
 def test_underflow_guard_and_zero_v(dev, oracle_mod, variant):
     """m0 = 0 (fa_tc_int8_b.cu:402): with all scores far below 0 the row sum underflows past the
