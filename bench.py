@@ -38,44 +38,64 @@ def flops(B, H, N, d):
     return 4.0 * B * H * N * N * d  # QK^T 2N^2d + PV 2N^2d per head (softmax excluded)
 
 
-def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=True):
-    lib = _lib.load()
-    vid = _lib.variant_id(variant)
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(x, dev):
+    """MAX of a host float over all ranks (the slowest rank defines the step)."""
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=True, dry_run=False):
+    """Time `steps` qmha_solve_ex calls on this rank's own shard (B sequences), bracketed by a
+    barrier + device synchronisation on both sides; the max over ranks is returned.
+    dry_run (CPU, gloo; launcher/rendezvous plumbing only): the step is a tensor copy."""
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     Q = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
     K = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
     V = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
     O = torch.empty_like(Q)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+    if dry_run:
+        lib = None
 
-    def step():
-        st = lib.qmha_solve_ex(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, H * d, H, vid, sptr)
-        _lib.check(st, variant)
+        def step():
+            O.copy_(Q)
+    else:
+        lib = _lib.load()
+        vid = _lib.variant_id(variant)
+        sptr = torch.cuda.current_stream(dev).cuda_stream
+
+        def step():
+            st = lib.qmha_solve_ex(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, H * d, H, vid, sptr)
+            _lib.check(st, variant)
 
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize(dev)
-    lib.qmha_profile_collect(None, None, None)  # drop anything recorded so far
-    lib.qmha_profile_enable(1 if profile else 0)
-    if world > 1:
+    _sync(dev)
+    if lib is not None:
+        lib.qmha_profile_collect(None, None, None)  # drop anything recorded so far
+        lib.qmha_profile_enable(1 if profile else 0)
+    if dist.is_initialized():
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
+    _sync(dev)
+    if dist.is_initialized():
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    lib.qmha_profile_enable(0)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     import ctypes
     main_ms, pre_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
-    lib.qmha_profile_collect(ctypes.byref(main_ms), ctypes.byref(n), ctypes.byref(pre_ms))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if lib is not None:
+        lib.qmha_profile_enable(0)
+        lib.qmha_profile_collect(ctypes.byref(main_ms), ctypes.byref(n), ctypes.byref(pre_ms))
     launches = max(1, n.value)
     return {
         "elapsed_s": elapsed,
@@ -83,6 +103,7 @@ def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=Tr
         "main_kernel_ms": main_ms.value / launches,
         "prepass_ms": pre_ms.value / launches,
         "launches": n.value,
+        "inputs": (Q, K, V),
         "O": O,
     }
 
@@ -114,18 +135,41 @@ def time_solve_calls(variant, B, H, N, d, dev, reps=3):
 
 
 def time_allgather(O, steps, dev, world):
-    out = torch.empty((world,) + tuple(O.shape), dtype=O.dtype, device=dev)
+    """The RCCL all-gather of every rank's output shard alone (ms per gather, max over ranks)."""
+    out = torch.empty((world * O.shape[0],) + tuple(O.shape[1:]), dtype=O.dtype, device=dev)
     dist.all_gather_into_tensor(out, O)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         dist.all_gather_into_tensor(out, O)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item()) * 1e3 / steps
+    return max_over_ranks(time.perf_counter() - t0, dev) * 1e3 / steps
+
+
+def time_solve_gather(variant, inputs, H, d, steps, dev, world, chunks, dry_run=False):
+    """Compute + all-gather per step, the gather of batch chunk c overlapped with the compute
+    of chunk c+1 (shard.solve_shard_gather); ms per step, max over ranks."""
+    from quantizedmha_amd.shard import solve_shard_gather
+    Q, K, V = inputs
+    batch = Q.shape[0] * world  # every rank holds an equal shard here
+    fn = (lambda q, k, v, dm, h, kern: q.clone()) if dry_run else None
+
+    def step():
+        return solve_shard_gather(Q, K, V, H * d, H, batch, variant, chunks=chunks, solve_fn=fn)
+
+    out = step()
+    _sync(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    _sync(dev)
+    dist.barrier()
+    ms = max_over_ranks(time.perf_counter() - t0, dev) * 1e3 / steps
+    assert out.shape[0] == batch
+    return ms
 
 
 def cpu_baseline(budget_s=20.0):
@@ -211,6 +255,22 @@ def pmc_traffic(variant, B, H, N, d):
     return None, None
 
 
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) outside a torch.distributed launcher: start the N rank processes (one
+    per GPU, rendezvous on 127.0.0.1) with torch.distributed.run as a CHILD process and return
+    its exit status.  Nothing in this parent process has touched the GPU (no HIP call, no
+    torch.cuda query), so the ranks own their devices from a clean state."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -226,30 +286,52 @@ def main():
     ap.add_argument("--no-solve-calls", action="store_true",
                     help="skip the one-solve-per-sequence timing (profiled runs: keeps its B=1 launches "
                          "out of the main kernel's rocprof average)")
-    ap.add_argument("--allgather", action="store_true", default=None,
-                    help="time the RCCL all-gather of per-shard outputs (default on when N>1)")
+    ap.add_argument("--no-refconfig", action="store_true",
+                    help="skip the reference's own configuration (include/config.h: N8192 d_model1024 h32)")
+    ap.add_argument("--gather-chunks", type=int, default=4,
+                    help="batch chunks of the compute+all-gather step (gather of chunk c overlaps chunk c+1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher plumbing only (CPU, gloo): spawn, rendezvous, barriers, max-over-ranks "
+                         "timing and the chunked all-gather, with a tensor copy as the step; no kernel, no value")
     a = ap.parse_args()
 
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world != a.gpus:
+        sys.stderr.write(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks\n")
+        sys.exit(2)
+    dry = a.dry_run
+    if dry:
+        dev = torch.device("cpu")
+        B, H, N, d = min(a.B, 4), min(a.H, 2), min(a.N, 128), a.d
+    else:
+        if not torch.cuda.is_available():
+            sys.stderr.write("bench.py: no GPU visible (the HIP kernels have no CPU path); --dry-run tests the launcher\n")
+            sys.exit(2)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    B, H, N, d = a.B, a.H, a.N, a.d
+        dev = torch.device("cuda", local_rank)
+        B, H, N, d = a.B, a.H, a.N, a.d
+    if launched:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if dry:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
-    r = run_variant(a.variant, B, H, N, d, a.steps, a.warmup, dev, rank, world)
+    r = run_variant(a.variant, B, H, N, d, a.steps, a.warmup, dev, rank, world, dry_run=dry)
     total_flops = flops(B, H, N, d) * world
     value = total_flops / r["elapsed_s"] * a.steps / 1e12
     peak = PEAKS.get(a.variant, INT8_PEAK_TOPS)
-    achieved = flops(B, H, N, d) / (r["main_kernel_ms"] * 1e-3) / 1e12
+    achieved = flops(B, H, N, d) / (r["main_kernel_ms"] * 1e-3) / 1e12 if r["main_kernel_ms"] > 0 else 0.0
     traffic, traffic_src = pmc_traffic(a.variant, B, H, N, d)
     hbm_alg = 16.0 * B * N * H * d  # fp32 Q, K, V read once + O written once (per call)
     res = {
         "metric": "attention-fwd TFLOPS + ms/call, B16 H16 N4096 d64 (fp16 & int8)",
-        "value": round(value, 3),
+        "value": None if dry else round(value, 3),
         "unit": "TFLOPS",
         "n_gpus": world,
         "steps": a.steps,
@@ -259,25 +341,39 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int8" if a.variant == "fa_tc_int8_b" else ("fp16" if a.variant == "fa_tc_v1a" else "fp32"),
-        "data": "synthetic N(0, 0.5^2) fp32 Q/K/V, torch.Generator seed 1234+rank, resident in HBM",
-        "config": {"workload": f"{a.variant} attention forward (BASELINE config 4{'/5' if world > 1 else ''})",
+        "data": ("dry run: launcher plumbing on CPU/gloo, tensor copy as the step (no kernel)" if dry else
+                 "synthetic N(0, 0.5^2) fp32 Q/K/V, torch.Generator seed 1234+rank, resident in HBM"),
+        "config": {"workload": f"{a.variant} attention forward (BASELINE config {'5' if world > 1 else '4'})",
                    "variant": a.variant, "B_per_gpu": B, "H": H, "N": N, "d": d, "d_model": H * d,
-                   "global_batch": B * world, "parallelism": f"batch-shard x{world} (no collective in step)"},
-        "roofline": {"bound": "mfma", "kernel": f"qmha_fa_{'int8' if a.variant == 'fa_tc_int8_b' else a.variant}",
-                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "algorithmic_flops_per_launch": flops(B, H, N, d),
-                     "main_kernel_ms": round(r["main_kernel_ms"], 4),
-                     "prepass_ms": round(r["prepass_ms"], 4),
-                     "hbm_algorithmic_bytes_per_call": hbm_alg},
+                   "global_batch": B * world,
+                   "parallelism": f"batch-shard x{world} (no collective in the timed step; all-gather reported "
+                                  f"separately)"},
     }
-    if world > 1 and a.allgather is not False:
+    if dry:
+        res["dry_run"] = True
+    else:
+        res["roofline"] = {"bound": "mfma", "kernel": f"qmha_fa_{'int8' if a.variant == 'fa_tc_int8_b' else a.variant}",
+                           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(achieved / peak, 4), "traffic": traffic,
+                           "traffic_source": traffic_src,
+                           "algorithmic_flops_per_launch": flops(B, H, N, d),
+                           "main_kernel_ms": round(r["main_kernel_ms"], 4),
+                           "prepass_ms": round(r["prepass_ms"], 4),
+                           "hbm_algorithmic_bytes_per_call": hbm_alg}
+    if dist.is_initialized():
         ag_ms = time_allgather(r["O"], max(3, a.steps // 2), dev, world)
-        res["allgather_ms"] = round(ag_ms, 4)
-        res["value_with_allgather"] = round(total_flops / ((r["ms_per_step"] + ag_ms) * 1e-3) / 1e12, 3)
+        sg_ms = time_solve_gather(a.variant, r["inputs"], H, d, max(3, a.steps // 2), dev, world,
+                                  a.gather_chunks, dry_run=dry)
+        res["allgather"] = {
+            "what": f"RCCL all-gather of every rank's [{B}, {N}, {H * d}] fp32 output shard into the global "
+                    f"[{B * world}, {N}, {H * d}] on every rank",
+            "allgather_ms": round(ag_ms, 4),
+            "step_with_allgather_ms": round(sg_ms, 4),
+            "chunks": a.gather_chunks,
+            "value_with_allgather": None if dry else round(total_flops / (sg_ms * 1e-3) / 1e12, 3),
+        }
     del r
-    if not a.no_siblings:
+    if not a.no_siblings and not dry:
         sib = {}
         for v in ("fa_tc_v1a", "fa"):
             Bs = B if v != "fa" else 8
@@ -291,17 +387,34 @@ def main():
                                              PEAKS[v], 4)}
             del rv
         res["siblings"] = sib
-    if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls:
+    if not a.no_refconfig and not dry and world == 1:
+        res["reference_config"] = reference_config(a.variant, dev, rank, world)
+    if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls and not dry:
         ms = time_solve_calls(a.variant, B, H, N, d, dev)
         res["solve_calls"] = {"pattern": f"{B} blocking solve() calls, one per sequence (reference usage)",
                               "ms_per_step": round(ms, 4), "tflops": round(flops(B, H, N, d) / (ms * 1e-3) / 1e12, 3)}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not dry:
         res["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def reference_config(variant, dev, rank, world):
+    """The reference's own compiled configuration (include/config.h:22-28: N=8192, d_model=1024,
+    h=32, so d=32) -- the shape of its published per-head times (README.md:19: 7.70 ms per head
+    for fa_tc_int8_b on an L4).  One sequence, all 32 heads in one call; per-head ms beside it."""
+    B, H, N, d = 1, 32, 8192, 32
+    rv = run_variant(variant, B, H, N, d, 10, 3, dev, rank, world)
+    pub = {"fa_tc_int8_b": 7.70}.get(variant)
+    return {"config": f"B{B} H{H} N{N} d{d} (include/config.h)",
+            "ms_per_call": round(rv["ms_per_step"], 4),
+            "ms_per_head": round(rv["ms_per_step"] / H, 5),
+            "main_kernel_ms": round(rv["main_kernel_ms"], 4),
+            "tflops": round(flops(B, H, N, d) / (rv["ms_per_step"] * 1e-3) / 1e12, 3),
+            "reference_ms_per_head_L4": pub}
 
 
 if __name__ == "__main__":

@@ -97,6 +97,17 @@ int qmha_quantize_int8(const float *X, int B, int N, int d_model, int h, int8_t 
  */
 int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int h, int head, int32_t *S);
 
+/*
+ * Test hook (the bit-exact int32 Q@K^T check, reference fa_tc_int8_b.cu:484,496,514):
+ * runs the PRODUCTION int8 schedule (same kernel template and flags as qmha_solve_ex, plus the
+ * FL_DUMP stores) and writes what that kernel itself computed: O as qmha_solve_ex would, the
+ * int32 S = Qi Ki^T of every (sequence, head) as its MFMAs produced it (accumulator bias
+ * removed) into S[B*h][N][N], its in-register int8 Q operand into Qi[B*h][N][d] and the Q
+ * group scales into sQ[B*h][N/32].  d = 64, N >= 64.  Device pointers; blocking.
+ */
+int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
+                            int h, int32_t *S, int8_t *Qi, float *sQ);
+
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused") -> id, or -1. */
 int qmha_variant_from_name(const char *name);
 const char *qmha_variant_name(int variant);

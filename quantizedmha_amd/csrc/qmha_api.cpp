@@ -403,6 +403,28 @@ int qmha_debug_qk_int32(const float* Q, const float* K, int N, int d_model, int 
     return QMHA_OK;
 }
 
+int qmha_debug_fa_int8_dump(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model,
+                            int h, int32_t* S, int8_t* Qi, float* sQ) {
+    int D = 0;
+    int st = check_shape(Q, K, V, O, B, N, d_model, h, QMHA_FA_TC_INT8_B, &D);
+    if (st != QMHA_OK) return st;
+    if (!S || !Qi || !sQ || D != 64 || N < 64) {
+        g_last_error = "debug dump: needs S/Qi/sQ buffers, d = 64 and N >= 64 (the pipelined kernel)";
+        return QMHA_ERR_INVALID;
+    }
+    const size_t need = qmha::int8_workspace_bytes(B, N, h, D);
+    void* ws = nullptr;
+    st = get_workspace(need, nullptr, &ws);
+    if (st != QMHA_OK) return st;
+    const qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
+    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, 1, B, N, h, D, d_model, nullptr, /*first_tensor=*/1),
+                 "quant_int8 launch");
+    QMHA_HIP_TRY(qmha::launch_fa_int8_dump(w, Q, O, B, N, h, D, d_model, qmha::QkDump{S, Qi, sQ}, nullptr),
+                 "fa_int8 dump launch");
+    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    return QMHA_OK;
+}
+
 int qmha_variant_from_name(const char* name) {
     if (!name) return -1;
     if (!std::strcmp(name, "fa")) return QMHA_FA;

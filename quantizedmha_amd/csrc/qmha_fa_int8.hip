@@ -222,7 +222,11 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 // ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
 //   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
 // ---------------------------------------------------------------------------------------
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64, FL_AQK = 128 };
+//   FL_DUMP     (pipe kernel) also store what the kernel itself computed: the int32 S^T of every
+//               tile (bias removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump:
+//               the bit-exact check of the production Q@K^T path; never the production launch)
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64, FL_AQK = 128,
+       FL_DUMP = 256 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -499,7 +503,7 @@ template <int D, int WAVES, int FL, int PAD = 0>
 __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
     static_assert(D == 64, "pipelined schedule is written for d = 64 (2 k-steps, 2 d-blocks)");
     constexpr int SG = 2, RING = 3;
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
@@ -522,9 +526,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 
     v4i qop[2];
     float cq = 0.0f;
+    constexpr bool DUMP = FL & FL_DUMP;
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
-        cq = quant_q_operand<D>(qrow, half, qop) * c_log2;
+        const float sq = quant_q_operand<D>(qrow, half, qop);
+        cq = sq * c_log2;
+        if constexpr (DUMP) {  // the Q operand as held in registers: lane (col, half), k-step s
+            int8_t* qd = dbg.Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
+#pragma unroll
+            for (int s = 0; s < D / 32; ++s) *reinterpret_cast<v4i*>(qd + 32 * s) = qop[s];
+            if (lane == 0) dbg.sQ[(size_t)bh * G + qg] = sq;
+        }
     } else {
         qop[0] = qop[1] = v4i{0, 0, 0, 0};
     }
@@ -697,6 +709,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
             if ((t >> 1) + 2 < nst)
                 issue_at((t >> 1) + 2, ph >= 0 ? ((((1 + ph) >> 1) + 2) % RING) : (((t >> 1) + 2) % RING));
+        }
+        if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (32x32 accumulator map)
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    sd[8 * (r >> 2) + 4 * half + (r & 3)] = MAGIC ? s_cur[r] - 0x4B400000 : s_cur[r];
+            }
         }
         // operand reads for this iteration's MFMAs
         v8h v00, v01, v10, v11;
@@ -967,7 +987,7 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
 
 template <int D, int WAVES, int FL, int PAD = 0>
 static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
-                                      int d_model, hipStream_t stream) {
+                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}) {
     const int G = N / QMHA_GROUP;
     if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
@@ -979,7 +999,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     constexpr int lds_pad = 0;
 #endif
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
     return hipGetLastError();
 }
 
@@ -1042,6 +1062,14 @@ hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O
         case 128: return fa_int8_d<128>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
+}
+
+// The production int8 schedule with FL_DUMP: same kernel template, same flags plus the stores
+// of what it computed (S^T per tile, Q operand, sQ).  Only the pipelined kernel (d = 64) has it.
+hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, QkDump dbg, hipStream_t stream) {
+    if (D != 64 || N / QMHA_GROUP < 2) return hipErrorInvalidValue;
+    return fa_int8_pipe_launch<64, 4, FL_MAGIC | FL_KFOLD | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream) {

@@ -34,6 +34,15 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream);
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream);
+// what the production int8 kernel computed (FL_DUMP instance): S [B*H][N][N] int32 (bias
+// removed), Qi [B*H][N][D] (its in-register Q operand), sQ [B*H][N/32]
+struct QkDump {
+    int32_t* S;
+    int8_t* Qi;
+    float* sQ;
+};
+hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, QkDump dbg, hipStream_t stream);
 
 // ---- FP16 (fa_tc_v1a) ------------------------------------------------------------------
 struct F16Workspace {

@@ -92,3 +92,24 @@ def debug_qk_int32(Q: torch.Tensor, K: torch.Tensor, d_model: int, num_heads: in
         st = _lib.load().qmha_debug_qk_int32(Qc.data_ptr(), Kc.data_ptr(), N, d_model, num_heads, head, S.data_ptr())
     _lib.check(st, "debug_qk_int32")
     return S
+
+
+def debug_fa_int8_dump(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int):
+    """Run the production int8 kernel with its FL_DUMP stores (test hook): returns (O, S, Qi, sQ)
+    with O as flash_solve computes it, S [B, h, N, N] int32 = the kernel's own Q@K^T
+    accumulators (bias removed), Qi [B, h, N, d] its in-register int8 Q operand, sQ [B, h, N/32]."""
+    if not (Q.is_cuda and K.is_cuda and V.is_cuda):
+        raise RuntimeError("Inputs must be CUDA tensors")
+    Qc, Kc, Vc = Q.contiguous(), K.contiguous(), V.contiguous()
+    B, N = _shape(Qc, d_model)
+    d = d_model // num_heads
+    O = torch.empty_like(Qc)
+    S = torch.empty((B, num_heads, N, N), dtype=torch.int32, device=Q.device)
+    Qi = torch.empty((B, num_heads, N, d), dtype=torch.int8, device=Q.device)
+    sQ = torch.empty((B, num_heads, N // 32), dtype=torch.float32, device=Q.device)
+    torch.cuda.synchronize(Q.device)
+    with torch.cuda.device(Qc.device):
+        st = _lib.load().qmha_debug_fa_int8_dump(Qc.data_ptr(), Kc.data_ptr(), Vc.data_ptr(), O.data_ptr(), B, N,
+                                                 d_model, num_heads, S.data_ptr(), Qi.data_ptr(), sQ.data_ptr())
+    _lib.check(st, "debug_fa_int8_dump")
+    return O, S, Qi, sQ

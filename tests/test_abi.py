@@ -145,10 +145,18 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     syms = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
     stubs = set(re.findall(r"__device_stub__(\w+?)ILi(\d+)E(\w*)", syms))
     per = {}
+    dumps = []
     for name, d, rest in stubs:
         if name.startswith("qmha_gemm"):
             continue
+        m = re.match(r"Li(\d+)ELi(\d+)E", rest) if name == "qmha_fa_int8_pipe_kernel" else None
+        if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
+            dumps.append((d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
+            continue
         per.setdefault((name, d), set()).add(rest)
+    assert dumps
+    for d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
+        assert per[("qmha_fa_int8_pipe_kernel", d)] == {twin}, (d, twin)
     assert per, syms[:2000]
     for (name, d), inst in per.items():
         limit = 2 if name == "qmha_quant_int8_kernel" else 1  # the V layout is a template argument
@@ -156,3 +164,22 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     blob = open(path, "rb").read()
     for env in (b"QMHA_INT8_CFG", b"QMHA_F16_CFG", b"QMHA_F32_CFG", b"QMHA_OVERLAP_CHUNKS", b"QMHA_INT8_ABL"):
         assert env not in blob, env
+
+
+def test_compiled_torch_ext_imports_with_reference_signature(built):
+    """The compiled `torch_ext` module (reference extensions/torch/torch_ext.cpp:45-57) imports
+    by its reference name, keeps the argument names/defaults and rejects non-GPU inputs with
+    the reference message before touching the device."""
+    import sys
+    import torch
+    sys.path.insert(0, LIB_DIR)
+    try:
+        import torch_ext
+    finally:
+        sys.path.pop(0)
+    doc = torch_ext.flash_solve.__doc__
+    assert "flash_solve(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model" in doc
+    assert "kernel: str = 'fa_tc_int8_b'" in doc
+    x = torch.zeros(64, 64)
+    with pytest.raises(RuntimeError, match="Inputs must be CUDA tensors"):
+        torch_ext.flash_solve(x, x, x, 64, 1)

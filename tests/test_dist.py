@@ -53,8 +53,16 @@ def _worker(rank, world, port, B, kernel, result_path):
         local = solve_sharded(Q, K, V, 128, 2, kernel, gather=False, solve_fn=_oracle_solve(oracle))
         start, stop = batch_shard(B, rank, world)
         assert local.shape[0] == stop - start
+        # per-rank shards (no rank holds the global batch), all-gather overlapped per chunk
+        sh = [t[start:stop].clone() for t in (Q, K, V)]
+        outs = {c: solve_sharded(*sh, 128, 2, kernel, batch=B, chunks=c, solve_fn=_oracle_solve(oracle))
+                for c in (1, 2, 3)}
+        mine = solve_sharded(*sh, 128, 2, kernel, batch=B, gather=False, solve_fn=_oracle_solve(oracle))
+        assert torch.equal(mine, local)
+        with pytest.raises(ValueError):  # a shard of the wrong size is refused, not mis-gathered
+            solve_sharded(Q, K, V, 128, 2, kernel, batch=B, solve_fn=_oracle_solve(oracle))
         if rank == 0:
-            torch.save({"out": out}, result_path)
+            torch.save({"out": out, **{f"chunked{c}": o for c, o in outs.items()}}, result_path)
     finally:
         dist.destroy_process_group()
 
@@ -70,11 +78,37 @@ def test_shard_gloo_world2(oracle_mod, tmp_path, B, kernel):
     path = str(tmp_path / "out.pt")
     mp.start_processes(_worker, args=(2, _free_port(), B, kernel, path), nprocs=2, join=True,
                        start_method="spawn")
-    out = torch.load(path, weights_only=True)["out"]
+    res = torch.load(path, weights_only=True)
     Q, K, V = _inputs(B, 64, 128)
     ref = _oracle_solve(oracle_mod)(Q, K, V, 128, 2, kernel)
-    assert out.shape == (B, 64, 128)
-    assert torch.equal(out, ref)  # sharding is exact: the same per-sequence computation
+    for key, out in res.items():
+        assert out.shape == (B, 64, 128), key
+        assert torch.equal(out, ref), key  # sharding is exact: the same per-sequence computation
+
+
+def test_bench_spawns_ranks_dry_run():
+    """`python bench.py --gpus 2` with no launcher spawns its own two ranks (torch.distributed.run,
+    127.0.0.1); --dry-run runs the plumbing on CPU/gloo.  Rank 0 prints one JSON line with
+    n_gpus == 2 and the chunked all-gather timing."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["dry_run"] is True and j["value"] is None
+    assert j["config"]["global_batch"] == 2 * j["config"]["B_per_gpu"]
+    assert j["allgather"]["step_with_allgather_ms"] > 0
+    # a launcher/--gpus mismatch is an error, not a silently mislabelled line
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r2 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                        capture_output=True, text=True, timeout=120, env=env2, cwd=root)
+    assert r2.returncode == 2 and "--gpus 2" in r2.stderr
 
 
 def test_gather_world1_passthrough():
@@ -86,6 +120,28 @@ def test_gather_world1_passthrough():
         assert gather_outputs(x, 1) is x
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_bench_torchrun_world1_gpu(tmp_path):
+    """The multi-GPU entry point on the GPU: torch.distributed.run, one rank, RCCL process
+    group, the HIP kernel, the all-gather legs (compute-only and chunked compute+gather)."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"), "--gpus", "1", "--steps", "2",
+           "--warmup", "1", "--B", "2", "--N", "512", "--no-siblings", "--no-cpu-baseline", "--no-refconfig"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert j["n_gpus"] == 1 and j["value"] > 0
+    assert j["allgather"]["allgather_ms"] > 0 and j["allgather"]["value_with_allgather"] > 0
 
 
 @pytest.mark.gpu

@@ -111,6 +111,35 @@ def test_int8_qk_int32_bitexact(dev, oracle_mod, N, d_model, h, head):
 # --------------------------------------------------------------------------------------
 # end-to-end parity, all variants
 # --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,N,h,heads", [(1, 64, 2, None), (2, 96, 1, None), (1, 256, 2, None),
+                                          (1, 4096, 2, None), (2, 4096, 16, [(0, 3), (1, 12)])])
+def test_production_qk_int32_bitexact(dev, oracle_mod, B, N, h, heads):
+    """The int32 Q@K^T of the PRODUCTION int8 kernel, bit for bit (fa_tc_int8_b.cu:484,496,514):
+    the FL_DUMP twin of the shipped schedule stores, per tile, the S^T it feeds its softmax
+    (magic-biased accumulator, bias removed), its in-register int8 Q operand (quant_q_operand)
+    and sQ.  Every one must equal the oracle's quantize_heads / qk_int32, and its O must equal
+    flash_solve's O bit for bit (the stores do not change the computation)."""
+    from quantizedmha_amd import torch_ext
+    d = 64
+    dm = h * d
+    Q, K, V = rand_inputs(50 + N + h, B, N, dm)
+    Q, K, V = (x.reshape(B, N, dm) for x in (Q, K, V))
+    Q[0, 5, :] *= 9.0  # one outlier row: a Q group whose scale is set by a single row
+    K[-1, N - 1, :d] = 0.0
+    tq, tk, tv = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (Q, K, V))
+    O, S, Qi, sQ = torch_ext.debug_fa_int8_dump(tq, tk, tv, dm, h)
+    ref_O = torch_ext.flash_solve(tq, tk, tv, dm, h, kernel="fa_tc_int8_b")
+    torch.cuda.synchronize()
+    assert torch.equal(O, ref_O)
+    for b, k in heads or [(b, k) for b in range(B) for k in range(h)]:
+        Qi_ref, sq_ref = oracle_mod.quantize_heads(Q[b], dm, h)
+        Ki_ref, _ = oracle_mod.quantize_heads(K[b], dm, h)
+        assert np.array_equal(Qi[b, k].cpu().numpy(), Qi_ref[0, k]), (b, k)
+        assert np.array_equal(sQ[b, k].cpu().numpy(), sq_ref[0, k]), (b, k)
+        S_ref = oracle_mod.qk_int32(Qi_ref[0, k], Ki_ref[0, k])
+        assert np.array_equal(S[b, k].cpu().numpy(), S_ref), (b, k)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("case", ["medium", "large"])
 def test_variant_vs_reference_golden(dev, oracle_mod, variant, case):
@@ -266,10 +295,25 @@ def test_jax_ext_raw_pointer_entry(dev, oracle_mod):
     assert np.abs(out.cpu().numpy() - ref).max() <= TOL_ORACLE["fa_tc_v1a"]
 
 
+def _slices_vs_oracle(oracle_fn, Q, K, V, out, d, slices, nthreads=16):
+    """Stack the (batch, head) slices as the heads of one [N, S*d] problem, run the oracle on
+    them in one multi-threaded call and return (gpu, oracle) as [N, S*d] arrays."""
+    def stack(x):
+        return np.concatenate([x[b, :, k * d:(k + 1) * d].cpu().numpy() for b, k in slices], axis=1)
+    q, kk, v, o = (stack(x) for x in (Q, K, V, out))
+    ref = oracle_fn(q, kk, v, len(slices) * d, len(slices), nthreads)
+    return o, ref
+
+
+# 16 (batch, head) slices of a 16 x 16 grid, one per batch element, heads spread so that the
+# workgroups they map to fall on all 8 XCDs through the launcher's block remap
+C_SLICES = [(b, (7 * b + 3) % 16) for b in range(16)]
+
+
 def test_full_baseline_config_sampled_heads(dev, oracle_mod):
-    """BASELINE C4 (B16 H16 N4096 d64, int8): run the whole call on the GPU, check two
-    (batch, head) slices against the oracle and every row's convexity (all-positive V
-    => outputs inside [min V, max V] of that head)."""
+    """BASELINE C4 (B16 H16 N4096 d64, int8): the whole call on the GPU; 16 (batch, head) slices
+    spread across the XCD remap against the oracle, every row's convexity (all-positive V =>
+    outputs inside [0, 1]) everywhere."""
     from quantizedmha_amd import torch_ext
     B, N, H, d = 16, 4096, 16, 64
     g = torch.Generator(device=dev).manual_seed(0)
@@ -280,11 +324,70 @@ def test_full_baseline_config_sampled_heads(dev, oracle_mod):
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert float(out.min()) >= 0.0 and float(out.max()) <= 1.0
-    for b, k in [(0, 0), (11, 13)]:
-        cols = slice(k * d, (k + 1) * d)
-        q, kk, v = (x[b, :, cols].cpu().numpy() for x in (Q, K, V))
-        ref = oracle_mod.fa_int8(q, kk, v, d, 1)
-        assert_parity("fa_tc_int8_b", out[b, :, cols].cpu().numpy(), ref)
+    got, ref = _slices_vs_oracle(oracle_mod.fa_int8, Q, K, V, out, d, C_SLICES)
+    assert_parity("fa_tc_int8_b", got, ref)
+
+
+def test_c3_fp16_full_config_sampled_heads(dev, oracle_mod):
+    """BASELINE C3 (fa_tc_v1a, fp16 MFMA, B16 H16 N4096 d64) at its own workload: the whole
+    call on the GPU, 16 (batch, head) slices against oracle fa_fp16 at 2e-4 (fa_tc_v1a.cu:222-413)."""
+    from quantizedmha_amd import torch_ext
+    B, N, H, d = 16, 4096, 16, 64
+    g = torch.Generator(device=dev).manual_seed(33)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_v1a")
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    got, ref = _slices_vs_oracle(oracle_mod.fa_fp16, Q, K, V, out, d, C_SLICES)
+    assert_parity("fa_tc_v1a", got, ref)
+
+
+def test_c2_fp32_full_config_all_heads(dev, oracle_mod):
+    """BASELINE C2 (fa, fp32 scalar, B8 H8 N1024 d64) at its own workload, every one of the 64
+    heads against oracle fa_fp32 at 1e-5 (fa.cu:211-400)."""
+    from quantizedmha_amd import torch_ext
+    B, N, H, d = 8, 1024, 8, 64
+    g = torch.Generator(device=dev).manual_seed(22)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa")
+    torch.cuda.synchronize()
+    ref = oracle_mod.fa_fp32(Q.cpu().numpy(), K.cpu().numpy(), V.cpu().numpy(), H * d, H, 16)
+    assert_parity("fa", out.cpu().numpy(), ref)
+
+
+def test_compiled_torch_ext_module(dev, oracle_mod):
+    """The compiled pybind module (quantizedmha_amd/csrc/torch_ext.cpp, the reference's
+    extensions/torch/torch_ext.cpp drop-in): `import torch_ext; torch_ext.flash_solve(...)`
+    unchanged, bit-identical to the ctypes mirror for every variant, 2-D and 3-D inputs,
+    the reference's errors and its unknown-kernel warning."""
+    import sys
+    import warnings
+    sys.path.insert(0, os.path.join(ROOT, "quantizedmha_amd", "lib"))
+    try:
+        import torch_ext as compiled
+    finally:
+        sys.path.pop(0)
+    from quantizedmha_amd import torch_ext as mirror
+    Q, K, V = (torch.from_numpy(x).to(dev) for x in rand_inputs(44, 2, 256, 256))
+    for variant in VARIANTS:
+        a = compiled.flash_solve(Q, K, V, 256, 4, variant)
+        b = mirror.flash_solve(Q, K, V, 256, 4, kernel=variant)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), variant
+    two_d = compiled.flash_solve(Q[1], K[1], V[1], 256, 4)  # reference form: [N, d_model], default kernel
+    assert torch.equal(two_d, mirror.flash_solve(Q, K, V, 256, 4)[1])
+    ref = oracle_mod.fa_int8(Q[1].cpu().numpy(), K[1].cpu().numpy(), V[1].cpu().numpy(), 256, 4)
+    assert_parity("fa_tc_int8_b", two_d.cpu().numpy(), ref)
+    with pytest.raises(RuntimeError, match="Inputs must be CUDA tensors"):
+        compiled.flash_solve(Q.cpu(), K, V, 256, 4)
+    with pytest.raises(RuntimeError, match="Q must be float32"):
+        compiled.flash_solve(Q.double(), K, V, 256, 4)
+    with pytest.raises(RuntimeError, match="divisible by d_model"):
+        compiled.flash_solve(Q, K, V, 255, 4)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        c = compiled.flash_solve(Q, K, V, 256, 4, "fa_tc_v2b")  # unknown -> warned, default kernel
+    assert torch.equal(c, mirror.flash_solve(Q, K, V, 256, 4))
 
 
 def test_driver_binary_end_to_end(dev, tmp_path):

@@ -8,6 +8,8 @@ Outputs (in-tree, git-ignored, shipped to the GPU box with the snapshot):
     quantizedmha_amd/lib/libqmha.so                 all C-ABI entry points (include/launchers.h)
     quantizedmha_amd/lib/libqmha_<variant>.so       `solve` bound to one kernel (reference Makefile KERNEL=)
     quantizedmha_amd/bin/qmha_profile               HIP C++ host driver (reference drivers/main.cu)
+    quantizedmha_amd/lib/torch_ext<EXT_SUFFIX>      compiled pybind module `torch_ext` (reference
+                                                    extensions/torch/torch_ext.cpp), linked to libqmha.so
 No CUDA, no hipify, no multi-backend dispatch: hipcc --offload-arch=gfx950 only.
 """
 import argparse
@@ -77,6 +79,31 @@ def compile_one(src, extra=()):
     return out
 
 
+def torch_ext_cmd(out, libqmha):
+    """Compile line of the compiled `torch_ext` module (host C++ only: hipcc as the C++ compiler,
+    PyTorch's headers and libraries, linked against libqmha.so with an $ORIGIN rpath)."""
+    import sysconfig
+    import torch
+    import torch.utils.cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda") + [sysconfig.get_paths()["include"], os.path.join(ROOT, "include")]
+    libs = ce.library_paths(device_type="cuda")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return ([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", "-DTORCH_EXTENSION_NAME=torch_ext", "-DUSE_ROCM",
+             f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-unused-result", "-Wno-deprecated-declarations"] +
+            [f"-I{d}" for d in inc] + [os.path.join(CSRC, "torch_ext.cpp"), "-o", out] + [f"-L{d}" for d in libs] +
+            ["-L", LIB, "-lqmha", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-ltorch_hip",
+             "-Wl,-rpath,$ORIGIN"] + [f"-Wl,-rpath,{d}" for d in libs])
+
+
+def build_torch_ext(libqmha):
+    import sysconfig
+    out = os.path.join(LIB, "torch_ext" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if newer(out, [os.path.join(CSRC, "torch_ext.cpp"), libqmha, os.path.join(ROOT, "include", "launchers.h"),
+                   __file__]):
+        run(torch_ext_cmd(out, libqmha))
+    return out
+
+
 def build(jobs=8, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(LIB, exist_ok=True)
@@ -95,11 +122,12 @@ def build(jobs=8, verbose=True):
         out = os.path.join(LIB, f"libqmha_{name}.so")
         if newer(out, [o, libqmha]):
             run([HIPCC, "-shared", "-fPIC", "-o", out, o, "-L", LIB, "-lqmha", "-Wl,-rpath,$ORIGIN"])
+    text = build_torch_ext(libqmha)
     driver = os.path.join(BIN, "qmha_profile")
     if newer(driver, drv_objs + [libqmha]):
         run([HIPCC, "-o", driver] + drv_objs + ["-L", LIB, "-lqmha", "-Wl,-rpath,$ORIGIN/../lib"])
     if verbose:
-        print("built:", libqmha, "+", len(shim_objs), "variant libs +", driver)
+        print("built:", libqmha, "+", len(shim_objs), "variant libs +", os.path.basename(text), "+", driver)
     return libqmha
 
 
