@@ -103,7 +103,7 @@ int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int 
  * FL_DUMP stores) and writes what that kernel itself computed: O as qmha_solve_ex would, the
  * int32 S = Qi Ki^T of every (sequence, head) as its MFMAs produced it (accumulator bias
  * removed) into S[B*h][N][N], its in-register int8 Q operand into Qi[B*h][N][d] and the Q
- * group scales into sQ[B*h][N/32].  d = 64, N >= 64.  Device pointers; blocking.
+ * group scales into sQ[B*h][N/32].  N >= 64.  Device pointers; blocking.
  */
 int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                             int h, int32_t *S, int8_t *Qi, float *sQ);

@@ -504,7 +504,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
-    static_assert(D == 64, "pipelined schedule is written for d = 64 (2 k-steps, 2 d-blocks)");
     constexpr int SG = 2, RING = 3;
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
@@ -524,7 +523,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     const int qg = qb * WAVES + wave;
     const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
 
-    v4i qop[2];
+    v4i qop[D / 32];
     float cq = 0.0f;
     constexpr bool DUMP = FL & FL_DUMP;
     if (active) {
@@ -538,7 +537,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             if (lane == 0) dbg.sQ[(size_t)bh * G + qg] = sq;
         }
     } else {
-        qop[0] = qop[1] = v4i{0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) qop[ks] = v4i{0, 0, 0, 0};
     }
     const int8_t* kbase = Ki + (size_t)bh * N * D;
     const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
@@ -601,45 +601,43 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     for (int r = 0; r < 16; ++r) magic_blk[r] = MAGIC ? 0x4B400000 : 0;
     if constexpr (MAGIC) asm volatile("" : "+v"(magic_blk));
 
-    v16f o0 = {}, o1 = {};      // O^T, d-blocks 0 and 1 (anchored)
+    // ---- MFMA schedule of one iteration, per head size.  An iteration issues the P@V MFMAs of
+    // tile t-1 (PV(m, ks): d-block m < MB, 16-key half ks) and the Q@K^T chain of tile t+1
+    // (QK(ks), ks < KS) between the six VALU chunks A..F of tile t's softmax; kSlot[c] MFMAs
+    // follow chunk c, in kOps order.  Every chained pair (same accumulator) is split by VALU.
+    constexpr int MB = D / 32;  // 32-wide d-blocks of O^T (PV accumulators)
+    constexpr int KS = D / 32;  // 32-deep k-steps of the i8 Q@K^T
+    constexpr int NOPS = 2 * MB + KS;
+    auto PVop = [](int m, int ks) { return 2 * m + ks; };
+    auto QKop = [](int ks) { return 1000 + ks; };
+    (void)PVop;
+    (void)QKop;
+    constexpr int kSlot64[6] = {1, 1, 1, 1, 1, 1};
+    constexpr int kOps64[6] = {0, 2, 1, 1000, 3, 1001};  // PV00 PV10 PV01 QK0 PV11 QK1
+    constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
+    constexpr int kOps32[3] = {0, 1, 1000};  // PV00 PV01 QK0
+    constexpr int kSlot128[6] = {2, 2, 2, 2, 2, 2};
+    constexpr int kOps128[12] = {0, 2, 4, 6, 1000, 1001, 1, 3, 5, 7, 1002, 1003};
+    auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
+    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]); };
+    static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
+    static_assert(NOPS == (D == 32 ? 3 : (D == 64 ? 6 : 12)), "MFMA schedule table");
+
+    v16f o[MB];                  // O^T, d-block m (anchored)
+#pragma unroll
+    for (int m = 0; m < MB; ++m) o[m] = v16f{};
     float m_run = 0.0f;          // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
     float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
-    // FL_AQK: Q@K^T accumulates in AGPRs (inline-asm MFMAs on s_acc, bias block in AGPRs) and S^T
-    // is read back by 16 v_accvgpr_read at the end of the iteration: a VGPR-form MFMA is
-    // serialised with VALU issue (profiles/r01/perturbation_int8.txt), an AGPR-form one is not.
-    // Needs the AGPR budget set in the IR ("amdgpu-agpr-alloc"), see tools/build.py.
-    constexpr bool AQK = FL & FL_AQK;
-    v16i s_acc, magic_a;
-    if constexpr (AQK) {
-        magic_a = magic_blk;
-        asm volatile("" : "+a"(magic_a));
-    }
-    auto qk0 = [&](const v4i& k, const v4i& q) {
-        if constexpr (AQK)
-            asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %3" : "=&a"(s_acc) : "v"(k), "v"(q), "a"(magic_a));
-        else
-            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, magic_blk, 0, 0, 0);
+    auto qk = [&](const v4i& kk, int ks) {
+        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
     };
-    auto qk1 = [&](const v4i& k, const v4i& q) {
-        if constexpr (AQK)
-            asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(s_acc) : "v"(k), "v"(q));
-        else
-            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(k, q, s_nxt, 0, 0, 0);
-    };
-    // S^T of the tile in flight into VGPRs (AQK); placed >= 50 instructions after its last MFMA
-    // (the 16-pass MFMA needs 18 wait states before a v_accvgpr_read of its result)
-    auto read_s = [&]() {
-        v16i r;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[i]) : "a"(s_acc[i]));
-        return r;
-    };
-    v8h pc0, pc1, pp0, pp1;      // P^T operand halves of tiles t (current) and t-1 (pending)
-    float scale_cur = 0.0f, scale_prev = 0.0f;
-    v16f a0, a1;                 // P@V accumulators of the pending tile
+    v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
+    float scale_prev = 0.0f;
+    v16f a[MB];                  // P@V accumulators of the pending tile
     constexpr bool EARLY = FL & FL_EARLY;
+    constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
     // FL_KFOLD (with FL_MAGIC): the exponent of key j is fma(A_j, c', -Kn) straight from the
     // biased accumulator A_j = 1.5*2^23 + S_j (as a float), with Kn = 1.5*2^23*c' + m.  c' is the
     // score scale rounded to 22 significant bits, so 1.5*2^23*c' is exact and the shift the
@@ -680,14 +678,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     issue(0);
     if (nst > 1) issue(1);
     qmha_dma_barrier();
-    qk0(kop_of(0, 0), qop[0]);
-    qk1(kop_of(0, 1), qop[1]);
-    if constexpr (AQK) {
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> v_accvgpr_read
-        s_cur = read_s();
-    } else {
-        s_cur = s_nxt;
-    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qk(kop_of(0, ks), ks);
+    s_cur = s_nxt;
     if constexpr (EARLY) head(s_cur, 0);
 
 #define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -701,10 +694,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
         const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
         const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
-        const int slot_n = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
         const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
-        auto vop_of = [&](int, int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
-        auto kop_of = [&](int, int ks) { return kop_at(slot_n, par_n, ks); };            // tile t+1
+        auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
         if (odd) {  // uniform
             qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
             if ((t >> 1) + 2 < nst)
@@ -718,21 +711,39 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                     sd[8 * (r >> 2) + 4 * half + (r & 3)] = MAGIC ? s_cur[r] - 0x4B400000 : s_cur[r];
             }
         }
-        // operand reads for this iteration's MFMAs
-        v8h v00, v01, v10, v11;
-        v4i k0, k1;
-        constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
+        // operand reads for this iteration's MFMAs (JIT: right before each MFMA instead)
+        v8h vv[MB][2];
+        v4i kk[KS];
         if constexpr (has_prev && !JIT) {
-            v00 = vop_of(t - 1, 0, 0);
-            v10 = vop_of(t - 1, 1, 0);
-            v01 = vop_of(t - 1, 0, 1);
-            v11 = vop_of(t - 1, 1, 1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
         }
         if constexpr (has_next && !JIT) {
-            k0 = kop_of(t + 1, 0);
-            k1 = kop_of(t + 1, 1);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) kk[ks] = kop(ks);
         }
         QMHA_FENCE();
+        // the MFMAs that follow VALU chunk c (compile-time after unrolling)
+        int op_i = 0;
+        auto mfmas = [&](int c) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j < slot_n(c)) {
+                    const int op = op_at(op_i++);
+                    if (op >= 1000) {
+                        const int ks = op - 1000;
+                        if (has_next) qk(JIT ? kop(ks) : kk[ks], ks);
+                    } else {
+                        const int m = op >> 1, ks = op & 1;
+                        if (has_prev)
+                            a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                          ks == 0 ? v16f{} : a[m], 0, 0, 0);
+                    }
+                }
+            }
+        };
         // ---- A: row max, running max, P-tile max (fa_tc_int8_b.cu:286-303, :359)
         if constexpr (!EARLY) {
             head(s_cur, t);
@@ -744,13 +755,13 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // overflow it); the pending tile t-1 carries its factor in scale_prev
         if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
             const float f = __builtin_amdgcn_exp2f(anchor - m_new);
-            o0 *= f;
-            o1 *= f;
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= f;
             l_run *= f;
             scale_prev *= f;
             anchor = m_new;
         }
-        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a0) : "v"(pp0), "v"(pp1)); else a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 0) : v00, pp0, v16f{}, 0, 0, 0); }
+        mfmas(0);
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
@@ -766,7 +777,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         QMHA_FENCE();
-        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a1) : "v"(pp0), "v"(pp1)); else a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 0) : v10, pp0, v16f{}, 0, 0, 0); }
+        mfmas(1);
         QMHA_FENCE();
         // ---- C: scores of rows 8..15
 #pragma unroll
@@ -779,20 +790,20 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         QMHA_FENCE();
-        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a0) : "v"(pp0), "v"(pp1)); else a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 0, 1) : v01, pp1, a0, 0, 0, 0); }
+        mfmas(2);
         QMHA_FENCE();
         // ---- D: p = exp2, rows 0..7
         float p[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_next) { if constexpr (PAD >= 20000) asm volatile("" : "=v"(s_nxt) : "v"(qop[0]), "v"(magic_blk)); else qk0(JIT ? kop_of(t + 1, 0) : k0, qop[0]); }
+        mfmas(3);
         QMHA_FENCE();
         // ---- E: p = exp2, rows 8..15
 #pragma unroll
         for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
         QMHA_FENCE();
-        if constexpr (has_prev) { if constexpr (PAD >= 10000 && (PAD / 10000) % 2 == 1) asm volatile("" : "=v"(a1) : "v"(pp0), "v"(pp1)); else a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop_of(t - 1, 1, 1) : v11, pp1, a1, 0, 0, 0); }
+        mfmas(4);
         QMHA_FENCE();
         // ---- F: Pi = rint(p/sP) (:317-321), carried as the f16 subnormal Pi * 2^-24:
         // fma(p, 1/sP, 1.5 * 2^23) rounds half-even to an integer whose float bits end in Pi,
@@ -803,35 +814,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         for (int r = 0; r < 8; ++r) {
             const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
             const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
-            if (r < 4) {
-                pc0[2 * r] = h2[0];
-                pc0[2 * r + 1] = h2[1];
-            } else {
-                pc1[2 * r - 8] = h2[0];
-                pc1[2 * r - 7] = h2[1];
-            }
+            pc[r >> 2][2 * (r & 3)] = h2[0];
+            pc[r >> 2][2 * (r & 3) + 1] = h2[1];
         }
         QMHA_FENCE();
-        if constexpr (has_next) { if constexpr (PAD >= 20000) asm volatile("" : "=v"(s_nxt) : "v"(qop[0]), "v"(magic_blk)); else qk1(JIT ? kop_of(t + 1, 1) : k1, qop[1]); }
+        mfmas(5);
         QMHA_FENCE();
-#ifdef QMHA_ABLATION
-        // perturbation (timing only): PAD % 100 extra independent v_add_f32 and (PAD % 10000) / 100 extra
-        // v_exp_f32 per tile on two dead registers (PAD >= 10000: MFMAs replaced, see below), to measure the marginal issue cost
-        if constexpr (PAD > 0) {
-            float z0 = __builtin_bit_cast(float, lane), z1 = z0;
-#pragma unroll
-            for (int i = 0; i < PAD % 100; ++i) {
-                if (i & 1) asm volatile("v_add_f32 %0, %0, %0" : "+v"(z1));
-                else asm volatile("v_add_f32 %0, %0, %0" : "+v"(z0));
-            }
-#pragma unroll
-            for (int i = 0; i < (PAD % 10000) / 100; ++i) {
-                if (i & 1) asm volatile("v_exp_f32 %0, %0" : "+v"(z1));
-                else asm volatile("v_exp_f32 %0, %0" : "+v"(z0));
-            }
-            asm volatile("" ::"v"(z0), "v"(z1));
-        }
-#endif
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
         const float rs = tree_sum16(p);
@@ -841,21 +829,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
         if constexpr (has_prev) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o0[r] = fmaf(a0[r], scale_prev, o0[r]);
+            for (int m = 0; m < MB; ++m)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o1[r] = fmaf(a1[r], scale_prev, o1[r]);
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
         }
         if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
         QMHA_FENCE();
-        scale_cur = scale_t;
         // rotate the pipeline
-        pp0 = pc0;
-        pp1 = pc1;
-        scale_prev = scale_cur;
-        if constexpr (has_next) {
-            if constexpr (AQK) s_cur = read_s();
-            else s_cur = s_nxt;
-        }
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        scale_prev = scale_t;
+        if constexpr (has_next) s_cur = s_nxt;
     };
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
@@ -877,30 +861,30 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // drain: P@V of the last tile
     {
         const int t = G - 1;
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 0, 0), pp0, v16f{}, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 1, 0), pp0, v16f{}, 0, 0, 0);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 0, 1), pp1, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, 1, 1), pp1, a1, 0, 0, 0);
-        o0 += a0 * scale_prev;
-        o1 += a1 * scale_prev;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int m = 0; m < MB; ++m)
+                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < MB; ++m) o[m] += a[m] * scale_prev;
     }
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
+    // lane (col, half) holds O^T rows d = 32 m + 8 g4 + 4 half + jj of query col
     if (active) {
         const float unanchor = __builtin_amdgcn_exp2f(anchor - m_run);
         const float l = half_swap_add(l_run) * unanchor;
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            v4f w0, w1;
+        for (int m = 0; m < MB; ++m)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                w0[jj] = ok ? (o0[4 * g4 + jj] * unanchor) / l : 0.0f;
-                w1[jj] = ok ? (o1[4 * g4 + jj] * unanchor) / l : 0.0f;
+            for (int g4 = 0; g4 < 4; ++g4) {
+                v4f w;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) w[jj] = ok ? (o[m][4 * g4 + jj] * unanchor) / l : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
             }
-            *reinterpret_cast<v4f*>(orow + 8 * g4) = w0;
-            *reinterpret_cast<v4f*>(orow + 32 + 8 * g4) = w1;
-        }
     }
 }
 
@@ -1003,6 +987,16 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     return hipGetLastError();
 }
 
+// Pipelined-kernel flags at d = 32 and d = 128 (A/B builds may override with -DQMHA_D32_FL=...).
+// d = 128: 4 d-blocks of O and of P@V accumulators -> 2 waves per SIMD, operands read at their MFMA
+#ifndef QMHA_D32_FL
+#define QMHA_D32_FL (FL_MAGIC | FL_KFOLD)
+#endif
+#ifndef QMHA_D128_FL
+#define QMHA_D128_FL (FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2)
+#endif
+constexpr int kD32Flags = QMHA_D32_FL, kD128Flags = QMHA_D128_FL;
+
 // Default geometry per head size (QMHA_INT8_CFG tuning alternatives: QMHA_ABLATION builds only).
 template <int D>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
@@ -1019,11 +1013,6 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, Qf, O, B, N, H, d_model, stream);
             case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, Qf, O, B, N, H, d_model, stream);
             case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, Qf, O, B, N, H, d_model, stream);
-            case 1008: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 8>(w, Qf, O, B, N, H, d_model, stream);
-            case 1016: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 16>(w, Qf, O, B, N, H, d_model, stream);
-            case 1032: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 32>(w, Qf, O, B, N, H, d_model, stream);
-            case 1400: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 400>(w, Qf, O, B, N, H, d_model, stream);
-            case 1800: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 800>(w, Qf, O, B, N, H, d_model, stream);
             case 11000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 10000>(w, Qf, O, B, N, H, d_model, stream);
             case 12000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 20000>(w, Qf, O, B, N, H, d_model, stream);
             case 13000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 30000>(w, Qf, O, B, N, H, d_model, stream);
@@ -1043,7 +1032,6 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9049: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY | FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
             case 9043: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
-            case 9045: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_AQK>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
@@ -1051,7 +1039,8 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
         // (KFOLD: -2 % against plain MAGIC on one box, profiles/r01/overlap_sweep.txt)
         return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
     }
-    return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
+    return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
@@ -1065,11 +1054,17 @@ hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O
 }
 
 // The production int8 schedule with FL_DUMP: same kernel template, same flags plus the stores
-// of what it computed (S^T per tile, Q operand, sQ).  Only the pipelined kernel (d = 64) has it.
+// of what it computed (S^T per tile, Q operand, sQ), at every head size.
 hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, QkDump dbg, hipStream_t stream) {
-    if (D != 64 || N / QMHA_GROUP < 2) return hipErrorInvalidValue;
-    return fa_int8_pipe_launch<64, 4, FL_MAGIC | FL_KFOLD | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    if (N / QMHA_GROUP < 2) return hipErrorInvalidValue;
+    switch (D) {  // the production flags of fa_int8_d, plus FL_DUMP
+        case 32: return fa_int8_pipe_launch<32, 4, kD32Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 64: return fa_int8_pipe_launch<64, 4, FL_MAGIC | FL_KFOLD | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 128:
+            return fa_int8_pipe_launch<128, 4, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream) {

@@ -111,16 +111,17 @@ def test_int8_qk_int32_bitexact(dev, oracle_mod, N, d_model, h, head):
 # --------------------------------------------------------------------------------------
 # end-to-end parity, all variants
 # --------------------------------------------------------------------------------------
-@pytest.mark.parametrize("B,N,h,heads", [(1, 64, 2, None), (2, 96, 1, None), (1, 256, 2, None),
-                                          (1, 4096, 2, None), (2, 4096, 16, [(0, 3), (1, 12)])])
-def test_production_qk_int32_bitexact(dev, oracle_mod, B, N, h, heads):
+@pytest.mark.parametrize("B,N,h,d,heads", [(1, 64, 2, 64, None), (2, 96, 1, 64, None), (1, 256, 2, 64, None),
+                                            (1, 4096, 2, 64, None), (2, 4096, 16, 64, [(0, 3), (1, 12)]),
+                                            (1, 160, 2, 32, None), (1, 8192, 32, 32, [(0, 0), (0, 31)]),
+                                            (2, 128, 2, 128, None), (1, 2048, 4, 128, [(0, 2)])])
+def test_production_qk_int32_bitexact(dev, oracle_mod, B, N, h, d, heads):
     """The int32 Q@K^T of the PRODUCTION int8 kernel, bit for bit (fa_tc_int8_b.cu:484,496,514):
     the FL_DUMP twin of the shipped schedule stores, per tile, the S^T it feeds its softmax
     (magic-biased accumulator, bias removed), its in-register int8 Q operand (quant_q_operand)
     and sQ.  Every one must equal the oracle's quantize_heads / qk_int32, and its O must equal
     flash_solve's O bit for bit (the stores do not change the computation)."""
     from quantizedmha_amd import torch_ext
-    d = 64
     dm = h * d
     Q, K, V = rand_inputs(50 + N + h, B, N, dm)
     Q, K, V = (x.reshape(B, N, dm) for x in (Q, K, V))
@@ -159,6 +160,8 @@ def test_variant_vs_reference_golden(dev, oracle_mod, variant, case):
     (1, 160, 256, 2, "uniform"),  # d=128, U[0,1) (the reference's profiling distribution)
     (3, 256, 128, 2, "uniform"),  # batch
     (1, 1024, 64, 1, "normal"),   # longer sequence
+    (2, 608, 96, 3, "normal"),    # d=32, N/32 = 19: ring period 6 + a remainder, partial workgroup
+    (1, 416, 256, 2, "normal"),   # d=128, N/32 = 13
 ])
 def test_variant_vs_oracle_random(dev, oracle_mod, variant, B, N, d_model, h, dist):
     Q, K, V = rand_inputs(10 + N + B, B, N, d_model, dist)
@@ -325,6 +328,21 @@ def test_full_baseline_config_sampled_heads(dev, oracle_mod):
     assert torch.isfinite(out).all()
     assert float(out.min()) >= 0.0 and float(out.max()) <= 1.0
     got, ref = _slices_vs_oracle(oracle_mod.fa_int8, Q, K, V, out, d, C_SLICES)
+    assert_parity("fa_tc_int8_b", got, ref)
+
+
+def test_reference_own_config_int8_sampled_heads(dev, oracle_mod):
+    """The reference's own compiled configuration (include/config.h:22-28: N=8192, d_model=1024,
+    h=32 -> d=32; the shape of its README.md:19 timing) through fa_tc_int8_b: heads spread over
+    the launch against the oracle, U[0,1) inputs (the reference's data.cu:16-22 distribution)."""
+    from quantizedmha_amd import torch_ext
+    N, H, d = 8192, 32, 32
+    g = torch.Generator(device=dev).manual_seed(8192)
+    Q, K, V = (torch.rand(1, N, H * d, device=dev, generator=g) for _ in range(3))
+    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_b")
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    got, ref = _slices_vs_oracle(oracle_mod.fa_int8, Q, K, V, out, d, [(0, 0), (0, 9), (0, 20), (0, 31)])
     assert_parity("fa_tc_int8_b", got, ref)
 
 

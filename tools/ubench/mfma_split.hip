@@ -16,13 +16,19 @@ typedef float v16f __attribute__((ext_vector_type(16)));
              "v_fma_f32 %8, %8, %16, %17\n\tv_fma_f32 %9, %9, %16, %17\n\tv_fma_f32 %10, %10, %16, %17\n\tv_fma_f32 %11, %11, %16, %17\n\t" \
              "v_fma_f32 %12, %12, %16, %17\n\tv_fma_f32 %13, %13, %16, %17\n\tv_fma_f32 %14, %14, %16, %17\n\tv_fma_f32 %15, %15, %16, %17"
 
-// FORM 0: MFMA D in AGPRs, 1: D in arch VGPRs
+// FORM 0: MFMA D in AGPRs, 1: D in arch VGPRs, 2: D and the A/B operands all in AGPRs
+// (no arch-VGPR port touched by the MFMA wave at all)
 template <int FORM>
 __device__ float mfma_wave(float seed) {
     v8h a = {(_Float16)seed, 1, 2, 3, 4, 5, 6, 7};
     v16f c0, c1;
+    if constexpr (FORM == 2) asm volatile("" : "+a"(a));
     for (int i = 0; i < ITERS; ++i) {
-        if constexpr (FORM == 0)
+        if constexpr (FORM == 2)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %2, 0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %2, 0\n\t"
+                         "v_mfma_f32_32x32x16_f16 %0, %2, %2, 0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %2, 0"
+                         : "=a"(c0), "=a"(c1) : "a"(a));
+        else if constexpr (FORM == 0)
             asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %2, 0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %2, 0\n\t"
                          "v_mfma_f32_32x32x16_f16 %0, %2, %2, 0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %2, 0"
                          : "=a"(c0), "=a"(c1) : "v"(a));
@@ -33,7 +39,7 @@ __device__ float mfma_wave(float seed) {
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     float r0, r1;
-    if constexpr (FORM == 0) {
+    if constexpr (FORM != 1) {
         asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r0) : "a"(c0[0]));
         asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r1) : "a"(c1[0]));
     } else {
@@ -94,14 +100,16 @@ float run(int M, int V, int NV) {
 
 int main() {
     std::printf("ns per slot per SIMD (slot = 1 MFMA 32x32x16 f16 on the MFMA wave + NV v_fma_f32 spread over V VALU waves)\n");
-    for (int form = 0; form < 2; ++form)
+    auto R = [](int form, int M, int V, int NV) {
+        return form == 0 ? run<0>(M, V, NV) : form == 1 ? run<1>(M, V, NV) : run<2>(M, V, NV);
+    };
+    const char* fname[3] = {"agpr", "vgpr", "all-agpr"};
+    for (int form = 0; form < 3; ++form)
         for (int NV : {8, 16, 32}) {
             for (int V : {1, 2, 3}) {
-                const float tm = form ? run<1>(1, 0, NV) : run<0>(1, 0, NV);
-                const float tv = form ? run<1>(0, V, NV) : run<0>(0, V, NV);
-                const float tb = form ? run<1>(1, V, NV) : run<0>(1, V, NV);
+                const float tm = R(form, 1, 0, NV), tv = R(form, 0, V, NV), tb = R(form, 1, V, NV);
                 std::printf("%s NV%-2d V%d  mfma %.2f  valu %.2f  both %.2f   (sum %.2f, max %.2f)\n",
-                            form ? "vgpr" : "agpr", NV, V, tm, tv, tb, tm + tv, tm > tv ? tm : tv);
+                            fname[form], NV, V, tm, tv, tb, tm + tv, tm > tv ? tm : tv);
             }
         }
     return 0;
