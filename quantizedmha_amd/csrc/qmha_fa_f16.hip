@@ -88,6 +88,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     const float* __restrict__ Qf, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     QMHA_ENABLE_AGPR_MFMA();
+    // the score scale lives in a VGPR: a VOP3 fma reading an SGPR issues at the slow rate
+    // (~4.3 instead of ~2.5 cycles per wave64 on gfx950, profiles/r02/ubench_valu_cost.txt)
+    asm volatile("" : "+v"(c_log2));
     constexpr int KS = D / 16;           // QK k-steps (K = 16)
     constexpr int MB = D / 32;           // PV d-blocks
     constexpr int RB = 2 * D;            // K row bytes

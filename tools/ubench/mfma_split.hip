@@ -49,33 +49,47 @@ __device__ float mfma_wave(float seed) {
     return r0 + r1;
 }
 
+#define R16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+#define I_EXP(i) "v_exp_f32 %" #i ", %" #i "\n\t"
+#define I_ADD(i) "v_add_f32 %" #i ", %" #i ", %16\n\t"
+#define I_MAX3(i) "v_max3_i32 %" #i ", %" #i ", %16, %17\n\t"
+#define I_PERM(i) "v_perm_b32 %" #i ", %" #i ", %16, %17\n\t"
+#define I_DPP(i) "v_max_i32_dpp %" #i ", %" #i ", %16 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+#define OUTS16 "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]), \
+               "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]), "+v"(f[12]), "+v"(f[13]), "+v"(f[14]), "+v"(f[15])
+// VOP: 0 v_fma_f32, 1 v_exp_f32, 2 v_add_f32, 3 v_max3_i32, 4 v_perm_b32, 5 v_max_i32_dpp
+template <int VOP>
 __device__ float valu_wave(float seed, int groups) {
     float f[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) f[j] = seed + j;
     const float x = seed * 0.5f, y = seed * 0.25f;
-    for (int i = 0; i < groups; ++i)
-        asm volatile(F16C : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
-                     "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]), "+v"(f[12]), "+v"(f[13]), "+v"(f[14]), "+v"(f[15])
-                     : "v"(x), "v"(y));
+    for (int i = 0; i < groups; ++i) {
+        if constexpr (VOP == 0) asm volatile(F16C : OUTS16 : "v"(x), "v"(y));
+        if constexpr (VOP == 1) asm volatile(R16(I_EXP) : OUTS16 : "v"(x), "v"(y));
+        if constexpr (VOP == 2) asm volatile(R16(I_ADD) : OUTS16 : "v"(x), "v"(y));
+        if constexpr (VOP == 3) asm volatile(R16(I_MAX3) : OUTS16 : "v"(x), "v"(y));
+        if constexpr (VOP == 4) asm volatile(R16(I_PERM) : OUTS16 : "v"(x), "v"(y));
+        if constexpr (VOP == 5) asm volatile(R16(I_DPP) : OUTS16 : "v"(x), "v"(y));
+    }
     float s = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) s += f[j];
     return s;
 }
 
-template <int FORM>
+template <int FORM, int VOP = 0>
 __global__ __launch_bounds__(1024) void k(float* out, float seed, int m_waves, int valu_groups) {
     const int wave = threadIdx.x >> 6;
     float r;
     if (wave < 4 * m_waves)
         r = mfma_wave<FORM>(seed);
     else
-        r = valu_wave(seed, valu_groups);
+        r = valu_wave<VOP>(seed, valu_groups);
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
-template <int FORM>
+template <int FORM, int VOP = 0>
 float run(int M, int V, int NV) {
     const int blocks = 256;
     const int threads = 256 * (M + V);
@@ -84,12 +98,12 @@ float run(int M, int V, int NV) {
     const int groups = V ? ITERS * 4 * NV / (16 * V) : 0;
     float* out;
     (void)hipMalloc(&out, (size_t)blocks * threads * 4);
-    hipLaunchKernelGGL((k<FORM>), dim3(blocks), dim3(threads), 0, 0, out, 1.0f, M, groups);
+    hipLaunchKernelGGL((k<FORM, VOP>), dim3(blocks), dim3(threads), 0, 0, out, 1.0f, M, groups);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((k<FORM>), dim3(blocks), dim3(threads), 0, 0, out, 1.0f, M, groups);
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((k<FORM, VOP>), dim3(blocks), dim3(threads), 0, 0, out, 1.0f, M, groups);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -112,5 +126,22 @@ int main() {
                             fname[form], NV, V, tm, tv, tb, tm + tv, tm > tv ? tm : tv);
             }
         }
+    // other VALU opcodes beside AGPR-form MFMAs (3 VALU waves per SIMD, 16 opcodes per MFMA)
+    const char* vname[6] = {"v_fma_f32", "v_exp_f32", "v_add_f32", "v_max3_i32", "v_perm_b32", "v_max_i32_dpp"};
+    auto RV = [](int vop, int M, int V, int NV) {
+        switch (vop) {
+            case 1: return run<0, 1>(M, V, NV);
+            case 2: return run<0, 2>(M, V, NV);
+            case 3: return run<0, 3>(M, V, NV);
+            case 4: return run<0, 4>(M, V, NV);
+            case 5: return run<0, 5>(M, V, NV);
+            default: return run<0, 0>(M, V, NV);
+        }
+    };
+    for (int vop = 0; vop < 6; ++vop) {
+        const float tm = RV(vop, 1, 0, 16), tv = RV(vop, 0, 3, 16), tb = RV(vop, 1, 3, 16);
+        std::printf("agpr + %-14s NV16 V3  mfma %.2f  valu %.2f  both %.2f   (sum %.2f, max %.2f)\n", vname[vop], tm, tv,
+                    tb, tm + tv, tm > tv ? tm : tv);
+    }
     return 0;
 }

@@ -38,6 +38,11 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 #define I_CVTPK(i) "v_cvt_pk_f16_f32 %" #i ", %" #i ", %16\n\t"
 #define I_RCP(i) "v_rcp_f32 %" #i ", %" #i "\n\t"
 #define I_MAX3I(i) "v_max3_i32 %" #i ", %" #i ", %16, %17\n\t"
+#define I_MULS(i) "v_mul_f32 %" #i ", %18, %" #i "\n\t"
+#define I_FMACS(i) "v_fmac_f32 %" #i ", %18, %16\n\t"
+#define I_ADDS(i) "v_add_f32 %" #i ", %18, %" #i "\n\t"
+#define I_CMPS(i) "v_cmp_lt_f32 vcc, %18, %" #i "\n\t"
+#define I_CMPV(i) "v_cmp_lt_f32 vcc, %16, %" #i "\n\t"
 #define I_FMA_MIX(i) "v_fma_mix_f32 %" #i ", %" #i ", %16, %17\n\t"
 
 #define P8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -50,14 +55,15 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 enum {
     OP_FMA, OP_FMAC, OP_ADD, OP_MUL, OP_EXP, OP_MAX, OP_MAX3, OP_MAXI, OP_PERM, OP_CVT, OP_MOV, OP_FMAAK, OP_DPP, OP_PL,
     OP_SUB, OP_ADDU, OP_FMAS, OP_CVTPK, OP_RCP, OP_MAX3I, OP_FMAMIX, OP_PKFMA, OP_PKFMAB, OP_PKADD, OP_PKMUL, OP_PKMOV,
-    OP_MFMA16, OP_MFMA8, OP_N
+    OP_MULS, OP_FMACS, OP_ADDS, OP_CMPS, OP_CMPV, OP_MFMA16, OP_MFMA8, OP_N
 };
 static const char* kNames[OP_N] = {
     "v_fma_f32", "v_fmac_f32", "v_add_f32", "v_mul_f32", "v_exp_f32", "v_max_f32", "v_max3_f32", "v_max_i32",
     "v_perm_b32", "v_cvt_f32_i32", "v_mov_b32", "v_fmaak_f32", "v_max_i32_dpp", "v_permlane32_swap", "v_sub_f32",
     "v_add_u32", "v_fma_f32 (sgpr)", "v_cvt_pk_f16_f32", "v_rcp_f32", "v_max3_i32", "v_fma_mix_f32", "v_pk_fma_f32",
-    "v_pk_fma_f32 bcast", "v_pk_add_f32", "v_pk_mul_f32", "v_pk_mov_b32", "mfma_f32_32x32x16_f16",
-    "mfma_i32_32x32x32_i8"};
+    "v_pk_fma_f32 bcast", "v_pk_add_f32", "v_pk_mul_f32", "v_pk_mov_b32", "v_mul_f32 (sgpr, vop2)",
+    "v_fmac_f32 (sgpr, vop2)", "v_add_f32 (sgpr, vop2)", "v_cmp_lt_f32 (sgpr)", "v_cmp_lt_f32 (vgpr)",
+    "mfma_f32_32x32x16_f16", "mfma_i32_32x32x32_i8"};
 
 template <int OP>
 __device__ float body(float seed, float sx) {
@@ -97,6 +103,11 @@ __device__ float body(float seed, float sx) {
         if constexpr (OP == OP_RCP) ASM16(I_RCP);
         if constexpr (OP == OP_MAX3I) ASM16(I_MAX3I);
         if constexpr (OP == OP_FMAMIX) ASM16(I_FMA_MIX);
+        if constexpr (OP == OP_MULS) ASM16(I_MULS);
+        if constexpr (OP == OP_FMACS) ASM16(I_FMACS);
+        if constexpr (OP == OP_ADDS) ASM16(I_ADDS);
+        if constexpr (OP == OP_CMPS) asm volatile(R16(I_CMPS) : OUTS16 : "v"(x), "v"(y), "s"(sx) : "vcc");
+        if constexpr (OP == OP_CMPV) asm volatile(R16(I_CMPV) : OUTS16 : "v"(x), "v"(y), "s"(sx) : "vcc");
         if constexpr (OP == OP_PKFMA) { ASM8P(I_PKFMA); ASM8P(I_PKFMA); }
         if constexpr (OP == OP_PKFMAB) { ASM8P(I_PKFMAB); ASM8P(I_PKFMAB); }
         if constexpr (OP == OP_PKADD) { ASM8P(I_PKADD); ASM8P(I_PKADD); }
