@@ -11,7 +11,7 @@ for ctr in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
            "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-siblings ${BENCH_ARGS} > $OUT/pmc$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-siblings --no-refconfig ${BENCH_ARGS} > $OUT/pmc$i.log 2>&1
   rc=$?; echo "pmc $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/pmc$i.log; exit $rc; fi
 done

@@ -66,7 +66,10 @@ def main():
             print(f"  = {n:30s} {v:.6g}")
         res[short(k)] = {"counters": c, "derived": der}
     if a.json_out:
-        main_k = [k for k in res if "fa_" in k and "kernel" in k]
+        # the main kernel of the shape's head size: template argument d (mangled ILi<d>E or <d, ...>)
+        dd = a.shape[3] if a.shape else None
+        main_k = [k for k in res if "fa_" in k and "kernel" in k and
+                  (dd is None or f"ILi{dd}E" in k or f"<{dd}," in k)]
         j = {"source": a.dir, "kernels": res}
         if main_k and a.shape:
             d = res[main_k[0]]["derived"]

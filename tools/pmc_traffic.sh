@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-siblings --variant $VAR --B $B --H $H --N $N --d $D > $OUT/pmc$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-siblings --no-refconfig --variant $VAR --B $B --H $H --N $N --d $D > $OUT/pmc$i.log 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/pmc$i.log; exit $rc; fi
 done
