@@ -18,9 +18,10 @@
 
 #define QMHA_GROUP 32
 
-// MFMA accumulators in AGPRs.  On gfx950 a VALU stream overlaps another wave's MFMA stream
-// only when the MFMA's C/D operands live in AGPRs (tools/ubench/mfma_coexec.hip: v_fma_f32 beside
-// 32x32x16 MFMAs 0.35 ms with AGPR accumulators vs 0.52 ms with VGPR ones = no overlap).  The
+// MFMA accumulators in AGPRs (A/B builds only).  r01 read tools/ubench/mfma_coexec.hip as "a VALU
+// stream overlaps another wave's MFMAs only with AGPR accumulators"; r02's mfma_split.hip shows
+// MFMA and VALU issue cycles ADD on a SIMD in every form once the VALU side is saturated
+// (profiles/r02/ubench_mfma_split*.txt), so production builds keep -amdgpu-mfma-vgpr-form.  The
 // compiler selects the AGPR form only for functions that may use AGPRs, which this empty
 // clobber declares; the build drops -amdgpu-mfma-vgpr-form when QMHA_MFMA_AGPR is set.
 #ifdef QMHA_MFMA_AGPR
@@ -58,6 +59,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef _Float16 v8h __attribute__((ext_vector_type(8)));
 typedef _Float16 v2h __attribute__((ext_vector_type(2)));
 typedef float v2f __attribute__((ext_vector_type(2)));
+typedef _Float16 v4h __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 // --------------------------------------------------------------------------
 // MFMA accumulator maps (gfx950, every 32x32 shape):
@@ -195,4 +198,42 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int q = nwg / 8, r = nwg % 8;
     const int xcd = orig % 8, slot = orig / 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+// --------------------------------------------------------------------------
+// Pre-pass writer of one 32-row group of V as the f16 V^T MFMA operand ([D][32 slots] f16, kv
+// slots in kv_of_slot_f16 order), shared by the int8 (QUANT: the quantised integers) and the
+// fp16 (RNE f16 values) pre-passes.  Lane (rq, c4) = (lane / (D/4), lane % (D/4)) holds the
+// D/8 CONSECUTIVE rows rq*D/8 .. of columns 4 c4 .. 4 c4 + 3 (x[i] = row rq*D/8 + i), loaded
+// as coalesced 16-byte pieces.  Consecutive kv rows 4a..4a+3 are 4 consecutive slots, so each
+// column goes to this wave's LDS tile T (D rows of PITCH bytes) as 8-byte pieces; the tile is
+// read back in 8-byte pieces and stored to dst as whole 16-byte lines.
+// --------------------------------------------------------------------------
+constexpr int QMHA_VT_PITCH = 64 + 8;  // bytes per d-row of the LDS tile (8-byte pad)
+template <int D, bool QUANT>
+__device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
+    constexpr int C4 = D / 4, NI = D / 8;
+    const int rq = lane / C4, c4 = lane % C4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int d = 4 * c4 + c;
+#pragma unroll
+        for (int a = 0; a < NI / 4; ++a) {  // kv rows NI rq + 4a .. +3 -> 4 consecutive slots
+            v4h h;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                h[e] = QUANT ? (_Float16)qmha_quant_i8(x[4 * a + e][c], inv) : (_Float16)x[4 * a + e][c];
+            *reinterpret_cast<v4h*>(T + d * QMHA_VT_PITCH + 2 * slot_of_kv_f16(NI * rq + 4 * a)) = h;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    constexpr int LINES = D * 64 / 16;  // 16-byte output lines of the group
+#pragma unroll
+    for (int u = lane; u < LINES; u += 64) {
+        const int d = u >> 2, q = u & 3;
+        const v2i lo = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 16 * q);
+        const v2i hi = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 16 * q + 8);
+        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
+    }
 }

@@ -33,20 +33,18 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
     const int b = bh / H, k = bh % H;
     const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
     if (tensor == 2) {
-        // V^T operand order without an LDS transpose (see qmha_quant_int8_kernel): lane unit
-        // u = lane + 64 i writes the 8-slot chunk j = u / D of row d = u % D
+        // V^T operand order through a per-wave LDS transpose (vt_group_store, shared with the
+        // int8 pre-pass): coalesced 16-byte non-temporal loads of NI consecutive rows per lane
+        __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
         if (active) {
-            constexpr int UPL = D / 16;
-            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D;
-            _Float16* dst = Vt + ((size_t)bh * G + g) * (size_t)(32 * D);
+            const int rq = lane / C4, c4 = lane % C4;
+            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
+            v4f x[NI];
 #pragma unroll
-            for (int i = 0; i < UPL; ++i) {
-                const int u = lane + 64 * i, d = u % D, j = u / D;
-                v8h h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (_Float16)base[(size_t)kv_of_slot_f16(8 * j + e) * d_model + d];
-                *reinterpret_cast<v8h*>(dst + d * 32 + 8 * j) = h;
-            }
+            for (int i = 0; i < NI; ++i)
+                x[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
+            vt_group_store<D, false>(vtr[wave], x, 1.0f, lane,
+                                     reinterpret_cast<char*>(Vt + ((size_t)bh * G + g) * (size_t)(32 * D)));
         }
         return;
     }
@@ -55,13 +53,13 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
     if (active) {
         const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
 #pragma unroll
-        for (int i = 0; i < NI; ++i) v[i] = *reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model);
+        for (int i = 0; i < NI; ++i)
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
     }
     if (active) {  // Q, K: f16 rows
         _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            typedef _Float16 v4h __attribute__((ext_vector_type(4)));
             v4h hv;
 #pragma unroll
             for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)

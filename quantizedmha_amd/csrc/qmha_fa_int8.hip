@@ -38,6 +38,14 @@ namespace qmha {
 // log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
 static constexpr float kLog2e = 1.4426950408889634f;
 
+#ifndef QMHA_PRE_NT
+#define QMHA_PRE_NT 1
+#endif
+#if QMHA_PRE_NT
+#define QMHA_PRE_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define QMHA_PRE_LOAD(p) (*(p))
+#endif
 // ---------------------------------------------------------------------------------------
 // Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
 // One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
@@ -66,38 +74,32 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
 
     if (tensor == 2 && v_mode == 1) {
-        // V straight into the f16 V^T operand order without an LDS transpose: lane unit
-        // u = lane + 64 i owns output chunk (d = u % D, slot chunk j = u / D), i.e. 8 values
-        // V[kv_of_slot_f16(8j + e)][d]; for a fixed (i, e) the lanes read consecutive d of one
-        // row (coalesced).  (The former LDS transpose ran into 16-way bank conflicts.)
-        constexpr int UPL = D / 16;  // units per lane
-        float x[UPL][8];
+        // V into the f16 V^T operand order ([d][32 slots] f16 per group) through a per-wave LDS
+        // transpose: coalesced 16-byte loads (instruction i covers rows i, NI+i, ...: 256-byte row
+        // segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns 4 c4..4 c4+3.  In the
+        // slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots (kv_of_slot_f16), so
+        // each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile is read back
+        // in 8-byte pieces and stored as 16-byte lines.  Loads are non-temporal: fp32 K/V are
+        // read exactly once per call.
+        __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
+        const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
+        v4f x[NI];
         float amax = 0.0f;
         if (active) {
-            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D;
+            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
 #pragma unroll
-            for (int i = 0; i < UPL; ++i) {
-                const int u = lane + 64 * i, d = u % D, j = u / D;
+            for (int i = 0; i < NI; ++i) {
+                x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    x[i][e] = base[(size_t)kv_of_slot_f16(8 * j + e) * d_model + d];
-                    amax = fmaxf(amax, fabsf(x[i][e]));
-                }
+                for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
             }
         }
         amax = wave_max64(amax);
         const float sc = qmha_scale_from_absmax(amax);
         const float inv = 1.0f / sc;
         if (active) {
-            _Float16* dst = static_cast<_Float16*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
-#pragma unroll
-            for (int i = 0; i < UPL; ++i) {
-                const int u = lane + 64 * i, d = u % D, j = u / D;
-                v8h h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (_Float16)qmha_quant_i8(x[i][e], inv);
-                *reinterpret_cast<v8h*>(dst + d * 32 + 8 * j) = h;
-            }
+            vt_group_store<D, true>(vtr[wave], x, inv, lane,
+                                    static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
             if (lane == 0) sV[item] = sc;
         }
         return;
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
         const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            v[i] = *reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model);
+            v[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
 #pragma unroll
             for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
         }
