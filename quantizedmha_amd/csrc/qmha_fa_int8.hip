@@ -227,18 +227,8 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //   FL_DUMP     (pipe kernel) also store what the kernel itself computed: the int32 S^T of every
 //               tile (bias removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump:
 //               the bit-exact check of the production Q@K^T path; never the production launch)
-//   FL_UPD      (pipe kernel, KFOLD) a tile in which some row's running max moves has P-tile max
-//               exp(0) = 1 exactly in the reference (fa_tc_int8_b.cu:296-303,359), so sP = 1/127 with no
-//               cross-lane reduction; a tile in which none moves keeps every row's 2^(m - anchor)
-//   FL_PKO      (pipe kernel) the O update as packed fp32 (v_pk_fma_f32, two d-rows per instruction)
-#ifndef QMHA_UPD_MODE
-#define QMHA_UPD_MODE 0
-#endif
-#ifndef QMHA_UPD_E
-#define QMHA_UPD_E 1
-#endif
-enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64, FL_AQK = 128,
-       FL_DUMP = 256, FL_UPD = 512, FL_PKO = 1024 };
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
+       FL_DUMP = 256 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -647,7 +637,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     };
     v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
     float scale_prev = 0.0f;
-    float e_run = 1.0f;          // (FL_UPD) 2^(m - anchor) of the last tile
     v16f a[MB];                  // P@V accumulators of the pending tile
     constexpr bool EARLY = FL & FL_EARLY;
     constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
@@ -664,11 +653,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // runs at the end of the previous iteration, in one scheduling region with that
     // iteration's O update, so its latency chain interleaves with independent work
     float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f;
-    constexpr bool UPD = FL & FL_UPD;
-    static_assert(!UPD || (KFOLD && !EARLY), "FL_UPD is written for the KFOLD head");
-    bool h_any = true;  // (FL_UPD) some row of the tile moves its running max
-    // sP and 1/sP of a tile whose P max is exactly 1 (the reference's max(1/127, 1e-8), 1/sP)
-    const float sp_one = fmaxf(div127_fast(1.0f), 1e-8f), invp_one = rcp_fast(sp_one);
     auto head = [&](const v16i& s, int t) {
         float c = cq * skb[t];
         const int mxi = half_swap_max_i(tree_max16_i(s));
@@ -687,28 +671,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             xmax = fmaf(mx, c, -h_m);
         }
         h_c = c;
-        if constexpr (UPD) {
-            h_any = __builtin_amdgcn_ballot_w64(h_m > m_run) != 0;  // wave-uniform
-#if QMHA_UPD_MODE == 1  // skip only the P max reduction
-            float pmax = 1.0f;
-            if (!h_any) pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
-            h_sp = fmaxf(div127_fast(pmax), 1e-8f);
-            h_invp = rcp_fast(h_sp);
-#else
-            if (h_any) {
-                h_sp = sp_one;
-                h_invp = invp_one;
-            } else {
-                const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
-                h_sp = fmaxf(div127_fast(pmax), 1e-8f);
-                h_invp = rcp_fast(h_sp);
-            }
-#endif
-        } else {
-            const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
-            h_sp = fmaxf(div127_fast(pmax), 1e-8f);
-            h_invp = rcp_fast(h_sp);
-        }
+        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
+        h_sp = fmaxf(div127_fast(pmax), 1e-8f);
+        h_invp = rcp_fast(h_sp);
         if constexpr (KFOLD) h_invp *= h_f;
     };
 
@@ -790,7 +755,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
         // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
         // overflow it); the pending tile t-1 carries its factor in scale_prev
-        bool moved = h_any;  // (FL_UPD) 2^(m_new - anchor) differs from the previous tile's
         if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
             const float f = __builtin_amdgcn_exp2f(anchor - m_new);
 #pragma unroll
@@ -798,21 +762,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             l_run *= f;
             scale_prev *= f;
             anchor = m_new;
-            moved = true;
-        }
-        if constexpr (UPD) {
-#if QMHA_UPD_E
-            if (moved) e_run = __builtin_amdgcn_exp2f(m_new - anchor);
-#else
-            (void)moved;
-            e_run = __builtin_amdgcn_exp2f(m_new - anchor);
-#endif
         }
         mfmas(0);
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
-        const float e = UPD ? e_run : __builtin_amdgcn_exp2f(m_new - anchor);
+        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
         float x[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -875,16 +830,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float scale_t = sp * svb[t] * e * 16777216.0f;  // 2^24: P entries are Pi * 2^-24
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
         if constexpr (has_prev) {
-            if constexpr (FL & FL_PKO) {
-                const v16f sc = scale_prev - v16f{};  // splat
 #pragma unroll
-                for (int m = 0; m < MB; ++m) o[m] = __builtin_elementwise_fma(a[m], sc, o[m]);
-            } else {
+            for (int m = 0; m < MB; ++m)
 #pragma unroll
-                for (int m = 0; m < MB; ++m)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
-            }
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
         }
         if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
         QMHA_FENCE();
