@@ -346,6 +346,28 @@ def test_reference_own_config_int8_sampled_heads(dev, oracle_mod):
     assert_parity("fa_tc_int8_b", got, ref)
 
 
+def test_c5_global_batch_on_one_gpu(dev, oracle_mod):
+    """BASELINE C5's whole global batch (B=128 H16 N4096 d64, 8 GPUs x 16 in the driver's scaling
+    run) through one launch on one GPU, via the batch-shard entry point at world 1: a 65,536-
+    workgroup grid over 8.6 GB per tensor.  Sequences spread over the batch (so over the workspace
+    and the XCD remap) against the oracle; every output finite and inside [0, 1] (V in [0, 1))."""
+    from quantizedmha_amd.shard import solve_sharded
+    B, N, H, d = 128, 4096, 16, 64
+    g = torch.Generator(device=dev).manual_seed(128)
+    Q = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
+    K = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
+    V = torch.rand(B, N, H * d, device=dev, generator=g)
+    out = solve_sharded(Q, K, V, H * d, H, "fa_tc_int8_b")
+    torch.cuda.synchronize()
+    assert out.shape == (B, N, H * d)
+    assert bool(torch.isfinite(out).all()) and float(out.min()) >= 0.0 and float(out.max()) <= 1.0
+    got, ref = _slices_vs_oracle(oracle_mod.fa_int8, Q, K, V, out, d,
+                                 [(0, 0), (17, 5), (63, 15), (64, 1), (101, 9), (127, 12)])
+    assert_parity("fa_tc_int8_b", got, ref)
+    del Q, K, V, out
+    torch.cuda.empty_cache()
+
+
 def test_c3_fp16_full_config_sampled_heads(dev, oracle_mod):
     """BASELINE C3 (fa_tc_v1a, fp16 MFMA, B16 H16 N4096 d64) at its own workload: the whole
     call on the GPU, 16 (batch, head) slices against oracle fa_fp16 at 2e-4 (fa_tc_v1a.cu:222-413)."""
