@@ -6,7 +6,9 @@
 //   S[r][j]  = fmaf chain over k = 0..d-1 from 0 (matmul_warp_tiled, :63-86 under nvcc's
 //              default FMA contraction), then * (1/sqrt(d))          -> bit-identical S
 //   O[r][:] *= alpha;  O[r][c] += (fmaf chain over the tile's 32 kv of P*V)  (:93-94)
-// exp/sum use the GPU's expf, so O agrees with the oracle to ~1e-6, not bitwise.
+// exp is exp2(x * log2 e) on v_exp_f32 (2 VALU ops; OCML's expf is ~13 per element with its
+// range checks, and its SGPR constants run at the slow issue rate): p differs from the
+// reference's expf by ~1e-6 relative, so O agrees with the oracle to ~1e-6, not bitwise.
 //
 // One workgroup = 32 query rows of one (batch, head), 256 threads = 4 wave64; thread
 // (r = tid/8, c = tid%8) owns S[r][c + 8j] (j < 4) and O[r][c + 8j] (j < D/8).
@@ -14,6 +16,10 @@
 #include "qmha_kernels.hpp"
 
 namespace qmha {
+
+// e^x as 2^(x log2 e): the rounding of x log2 e costs |x| * 2^-24 relative (< 2e-6 for the
+// |x| < 30 a softmax sees before p underflows), v_exp_f32 itself ~1 ulp
+__device__ __forceinline__ float exp_e(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
 template <int D>
 __global__ __launch_bounds__(256) void qmha_fa_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K,
@@ -73,14 +79,14 @@ __global__ __launch_bounds__(256) void qmha_fa_f32_kernel(const float* __restric
         float rs = 0.0f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float p = expf(s[j] - mx);  // fa.cu:167
+            const float p = exp_e(s[j] - mx);  // fa.cu:167
             ps[r * 33 + c + 8 * j] = p;
             rs += p;
         }
         rs += __shfl_xor(rs, 1);
         rs += __shfl_xor(rs, 2);
         rs += __shfl_xor(rs, 4);
-        const float alpha = expf(m_prev - mx);  // fa.cu:187
+        const float alpha = exp_e(m_prev - mx);  // fa.cu:187
         l = fmaf(alpha, l, rs);                 // fa.cu:190
         m_prev = mx;
         __syncthreads();
@@ -207,14 +213,14 @@ __global__ __launch_bounds__(256) void qmha_fa_f32_v2_kernel(const float* __rest
             float rs = 0.0f;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                pv[j] = expf(sacc[i][j] - mx);  // fa.cu:167
+                pv[j] = exp_e(sacc[i][j] - mx);  // fa.cu:167
                 rs += pv[j];
             }
             *reinterpret_cast<v4f*>(&ps[(rp + 32 * i) * PS + 4 * c]) = pv;
             rs += __shfl_xor(rs, 1);
             rs += __shfl_xor(rs, 2);
             rs += __shfl_xor(rs, 4);
-            alpha[i] = expf(m_prev[i] - mx);  // fa.cu:187
+            alpha[i] = exp_e(m_prev[i] - mx);  // fa.cu:187
             l[i] = fmaf(alpha[i], l[i], rs);  // fa.cu:190
             m_prev[i] = mx;
         }
@@ -368,14 +374,14 @@ __global__ __launch_bounds__(NT) void qmha_fa_f32_v3_kernel(const float* __restr
             float rs = 0.0f;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                pv[j] = expf(sacc[i][j] - mx);  // fa.cu:167
+                pv[j] = exp_e(sacc[i][j] - mx);  // fa.cu:167
                 rs += pv[j];
             }
             *reinterpret_cast<v4f*>(&ps[(rp + RS * i) * PS + 4 * c]) = pv;
             rs += __shfl_xor(rs, 1);
             rs += __shfl_xor(rs, 2);
             rs += __shfl_xor(rs, 4);
-            alpha[i] = expf(m_prev[i] - mx);  // fa.cu:187
+            alpha[i] = exp_e(m_prev[i] - mx);  // fa.cu:187
             l[i] = fmaf(alpha[i], l[i], rs);  // fa.cu:190
             m_prev[i] = mx;
         }
