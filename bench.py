@@ -274,8 +274,10 @@ def spawn_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    # 30 warm-up calls: the clock ramps for the first ~20-30 back-to-back calls of a fresh process
+    # (per-call times 1.8 -> 1.47 ms on one box, tools/ramp.py -> profiles/r02/clock_ramp.txt)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--variant", default="fa_tc_int8_b", choices=list(_lib.VARIANTS))
     ap.add_argument("--B", type=int, default=16, help="sequences per GPU")
     ap.add_argument("--H", type=int, default=16)

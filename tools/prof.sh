@@ -18,7 +18,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 rc=$?; echo "rocprof trace rc=$rc"
 if [ $rc -ne 0 ]; then tail -20 $OUT/trace.log; exit $rc; fi
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+find $OUT/trace -name "*kernel_trace.csv" -exec cp {} $OUT/kernel_trace.csv \;
 head -20 $OUT/kernel_stats.csv
+# the int8 main kernel over bench.py's timed window (its default warm-up calls skipped)
+python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64" 30 50 | tee $OUT/trace_window.txt
 i=0
 for ctr in "$@"; do
   i=$((i+1))
