@@ -170,6 +170,36 @@ def test_variant_vs_oracle_random(dev, oracle_mod, variant, B, N, d_model, h, di
     assert_parity(variant, out, ref)
 
 
+def _sweep_shapes(seed, n):
+    """n random (B, N, H, d) with N a multiple of 32 from 32 to 2048 (odd group counts
+    included), d in {32, 64, 128}, H in 1..8, B in 1..5, sized so the oracle finishes fast."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        d = int(rng.choice([32, 64, 128]))
+        G = int(rng.integers(1, 65))
+        H = int(rng.integers(1, 9))
+        B = int(rng.integers(1, 6))
+        if B * H * (32 * G) ** 2 * d > 2e9:
+            continue
+        out.append((B, 32 * G, H, d))
+    return out
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_random_shape_sweep(dev, oracle_mod, variant):
+    """Property sweep: 10 random shapes per variant (every d, odd and even KV-group counts, batch
+    and head counts) against the oracle at the variant's tolerance."""
+    for i, (B, N, H, d) in enumerate(_sweep_shapes(77 + VARIANTS.index(variant), 10)):
+        Q, K, V = rand_inputs(1000 + i, B, N, H * d, "normal" if i % 2 else "uniform")
+        out = run(variant, Q, K, V, H * d, H, dev)
+        ref = oracle_for(oracle_mod, variant)(Q, K, V, H * d, H)
+        try:
+            assert_parity(variant, out, ref)
+        except AssertionError as e:
+            raise AssertionError(f"{variant} B{B} N{N} H{H} d{d}: {e}") from None
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_all_ones_driver_check(dev, oracle_mod, variant):
     """drivers/main.cu:73-101: all-ones input, every output 1.0 within max(1e-3, 1e-3*|ref|)."""
