@@ -471,6 +471,53 @@ def test_driver_binary_end_to_end(dev, tmp_path):
         assert '"check_random": "passed"' in r.stdout
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_solve_ws_caller_scratch_and_graph_capture(dev, variant):
+    """qmha_solve_ws (caller-owned scratch, no allocation or synchronisation inside): equal to
+    qmha_solve_ex bit for bit on a side stream, and capturable in a HIP graph (torch.cuda.CUDAGraph
+    on ROCm) whose replays follow new inputs written into the captured buffers."""
+    from quantizedmha_amd import _lib, torch_ext
+    lib = _lib.load()
+    B, N, H, d = 2, 1024, 8, 64
+    g = torch.Generator(device=dev).manual_seed(9)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    vid = _lib.variant_id(variant)
+    ws_bytes = lib.qmha_workspace_size(B, N, H * d, H, vid)
+    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
+
+    def call(out, stream):
+        st = lib.qmha_solve_ws(Q.data_ptr(), K.data_ptr(), V.data_ptr(), out.data_ptr(), B, N, H * d, H, vid,
+                               ws.data_ptr(), ws_bytes, stream.cuda_stream)
+        _lib.check(st, variant)
+
+    ref = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
+    torch.cuda.synchronize()
+    O = torch.empty_like(Q)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        call(O, side)
+    side.synchronize()
+    assert torch.equal(O, ref)
+    if ws_bytes:  # too small a workspace is refused, not overrun
+        st = lib.qmha_solve_ws(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, H * d, H, vid,
+                               ws.data_ptr(), ws_bytes - 1, side.cuda_stream)
+        assert st != 0
+    O2 = torch.zeros_like(Q)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        call(O2, torch.cuda.current_stream(dev))
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(O2, ref)
+    Q.mul_(0.75)
+    V.add_(0.25)
+    ref2 = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(O2, ref2) and not torch.equal(ref2, ref)
+
+
 @pytest.mark.parametrize("variant", ["fa_tc_int8_b", "fa_tc_v1a"])
 def test_overlap_chunks_bit_identical(dev, variant):
     """Batch-chunked pre-pass/main overlap (qmha_set_overlap_chunks) must not change a bit, and
