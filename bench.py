@@ -31,7 +31,8 @@ from quantizedmha_amd import _lib  # noqa: E402
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x bf16 2.5 PF; MI355X_MICROARCH.md)
 F16_PEAK_TFLOPS = 2500.0
 F32_VALU_PEAK_TFLOPS = 157.3
-PEAKS = {"fa_tc_int8_b": INT8_PEAK_TOPS, "fa_tc_v1a": F16_PEAK_TFLOPS, "fa": F32_VALU_PEAK_TFLOPS}
+PEAKS = {"fa_tc_int8_b": INT8_PEAK_TOPS, "fa_tc_v1a": F16_PEAK_TFLOPS, "fa": F32_VALU_PEAK_TFLOPS,
+         "unfused": F32_VALU_PEAK_TFLOPS}
 
 
 def flops(B, H, N, d):
@@ -377,11 +378,14 @@ def main():
     del r
     if not a.no_siblings and not dry:
         sib = {}
-        for v in ("fa_tc_v1a", "fa"):
+        # fa_tc_v1a at C3 (= the C4 shape), fa at C2, and the reference's unfused 3-kernel baseline
+        # (README.md:11, the fused-vs-unfused comparison) at the C4 shape
+        for v in ("fa_tc_v1a", "fa", "unfused"):
             Bs = B if v != "fa" else 8
             Hs = H if v != "fa" else 8
             Ns = N if v != "fa" else 1024
-            rv = run_variant(v, Bs, Hs, Ns, d, max(3, a.steps // 2), 2, dev, rank, world)
+            steps_v, warm_v = (max(3, a.steps // 2), 2) if v != "unfused" else (3, 1)
+            rv = run_variant(v, Bs, Hs, Ns, d, steps_v, warm_v, dev, rank, world)
             sib[v] = {"config": f"B{Bs} H{Hs} N{Ns} d{d}", "ms_per_step": round(rv["ms_per_step"], 4),
                       "tflops": round(flops(Bs, Hs, Ns, d) * world / (rv["ms_per_step"] * 1e-3) / 1e12, 3),
                       "main_kernel_ms": round(rv["main_kernel_ms"], 4),
