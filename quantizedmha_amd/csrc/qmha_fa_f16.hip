@@ -79,7 +79,9 @@ __device__ __forceinline__ int chunk_swz_h(int row) {
 // one 32-key tile at a time, Q@K^T of the next tile issued before the current softmax
 // (FL_PREFETCH).  One wave = one 32-row Q group.
 // ---------------------------------------------------------------------------------------
-enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4 };
+// F16_VPRE: the tile's V^T operands are read from LDS before its softmax, so the P@V MFMAs do
+// not wait on their LDS reads
+enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8 };
 
 template <int D, int WAVES, int SG, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f16_v2_kernel(
@@ -185,6 +187,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
     };
     // online softmax of one tile (fa_tc_v1a.cu:101-220) and O = alpha*O + P V (:207,:218)
     auto tile = [&](const char* L, int gi, const v16f& s) {
+        v8h vpre[MB][2];
+        if constexpr (FL & F16_VPRE) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int d = 32 * m + col;
+                    vpre[m][ks] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 +
+                                                                16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                }
+        }
         float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);  // max3 chain
 #pragma unroll
         for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[r]), s[r + 1]);
@@ -214,7 +227,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
             const char* vr = L + KBYTES + gi * 64 * D + d * 64;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                const v8h vop = (FL & F16_VPRE) ? vpre[m][ks]
+                                                : *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
                 o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
             }
         }
@@ -330,6 +344,9 @@ static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float
     return hipGetLastError();
 }
 
+#ifndef QMHA_F16_FL
+#define QMHA_F16_FL (F16_LB4 | F16_VPRE)  // V operands before the softmax: -1.7 % (profiles/r02/ab/f16_vpre)
+#endif
 template <int D>
 static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                            hipStream_t stream) {
@@ -350,7 +367,7 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
 #endif
     // default: v2 (LDS-DMA staging, per-tile softmax), 4 waves/SIMD budget (r01 A/B: 1.54 ms vs
     // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64)
-    return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
+    return fa_f16_v2_launch<D, 4, 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,
