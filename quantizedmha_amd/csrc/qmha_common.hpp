@@ -160,11 +160,12 @@ __device__ __forceinline__ float rcp_fast(float x) {
 }
 
 // Balanced-tree reductions of 16 register values (independent chains for ILP).
+// 16 values in 8 v_max3 / v_max (5 + 2 + 1)
 __device__ __forceinline__ int tree_max16_i(const v16i& s) {
     int a = max(max(s[0], s[1]), s[2]), b = max(max(s[3], s[4]), s[5]);
     int c = max(max(s[6], s[7]), s[8]), d = max(max(s[9], s[10]), s[11]);
     int e = max(max(s[12], s[13]), s[14]);
-    return max(max(max(a, b), max(c, d)), max(e, (int)s[15]));
+    return max(max(max(a, b), c), max(max(d, e), (int)s[15]));
 }
 __device__ __forceinline__ float tree_sum16(const float* p) {
     float a = (p[0] + p[1]) + (p[2] + p[3]), b = (p[4] + p[5]) + (p[6] + p[7]);

@@ -672,9 +672,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         }
         h_c = c;
         const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
-        h_sp = fmaxf(div127_fast(pmax), 1e-8f);
-        h_invp = rcp_fast(h_sp);
+        // sP = max(pmax / 127, 1e-8) as pm / 127 with pm = max(pmax, 127e-8), and 1/sP by one
+        // v_rcp: within ~2 ulp of the reference's rounded 1/sP, which moves a Pi only when p/sP
+        // lies that close to a .5 boundary (the same class as exp2 vs expf).  h_sp carries the
+        // 2^24 of the f16-subnormal P entries (Pi * 2^-24)
+        const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
+        h_invp = __builtin_amdgcn_rcpf(sp);
         if constexpr (KFOLD) h_invp *= h_f;
+        h_sp = sp * 16777216.0f;
     };
 
     issue(0);
@@ -827,7 +832,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float rs = tree_sum16(p);
         l_run = fmaf(rs, KFOLD ? e * h_f : e, l_run);
         m_run = m_new;
-        const float scale_t = sp * svb[t] * e * 16777216.0f;  // 2^24: P entries are Pi * 2^-24
+        const float scale_t = sp * svb[t] * e;  // sp carries 2^24: P entries are Pi * 2^-24
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
         if constexpr (has_prev) {
 #pragma unroll

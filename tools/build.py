@@ -64,8 +64,10 @@ def header_deps():
 
 # per-source flags: the int8 softmax is written as scalar fp32 chains on purpose; SLP-packing
 # them into v_pk_* needs register pairs the exp results do not land in (a v_mov per pair)
-FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize"] + os.environ.get("QMHA_INT8_FLAGS", "").split(),
-              "qmha_fa_f16.hip": os.environ.get("QMHA_F16_FLAGS", "").split()}
+# -fno-honor-nans: fmaxf on MFMA results and running maxima otherwise gets a canonicalising
+# v_max (x, x) in front of it (5 per fp16 tile; scores here are finite by construction)
+FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize", "-fno-honor-nans"] + os.environ.get("QMHA_INT8_FLAGS", "").split(),
+              "qmha_fa_f16.hip": ["-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split()}
 
 
 def compile_one(src, extra=()):
