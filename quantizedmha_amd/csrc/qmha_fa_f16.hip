@@ -361,6 +361,10 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
             case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
             case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, Qf, O, B, N, H, d_model, stream);
+            case 427: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_VPRE | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 447: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE>(w, Qf, O, B, N, H, d_model, stream);
+            case 448: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 429: return fa_f16_v2_launch<D, 4, 2, F16_VPRE>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
     }
