@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 from quantizedmha_amd import _lib  # noqa: E402
 
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x bf16 2.5 PF; MI355X_MICROARCH.md)
 F16_PEAK_TFLOPS = 2500.0
 F32_VALU_PEAK_TFLOPS = 157.3
@@ -395,6 +396,9 @@ def main():
         res["siblings"] = sib
     if not a.no_refconfig and not dry and world == 1:
         res["reference_config"] = reference_config(a.variant, dev, rank, world)
+    if not a.no_siblings and not dry and world == 1:
+        res["quantize_int8"] = time_quantize_int8(B, H, N, d, dev)
+        res["torch_ext"] = time_torch_ext(B, H, N, d, dev)
     if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls and not dry:
         ms = time_solve_calls(a.variant, B, H, N, d, dev)
         res["solve_calls"] = {"pattern": f"{B} blocking solve() calls, one per sequence (reference usage)",
@@ -406,6 +410,70 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_quantize_int8(B, H, N, d, dev, steps=20):
+    """The standalone int8 quantisation op (qmha_quantize_int8: the reference's
+    fp32_to_int8sram, fa_tc_int8_b.cu:33-152, over whole tensors) on one C4-shaped fp32 tensor,
+    row layout and V^T-operand layout.  HBM-bound: algorithmic bytes = fp32 in + int8 out + one
+    fp32 scale per 32-row group; roofline against the ~8 TB/s HBM3E peak."""
+    lib = _lib.load()
+    g = torch.Generator(device=dev).manual_seed(7)
+    X = torch.randn(B, N, H * d, device=dev, generator=g) * 0.5
+    Xi = torch.empty(B * H * N * d, dtype=torch.int8, device=dev)
+    sc = torch.empty(B * H * (N // 32), dtype=torch.float32, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    out = {}
+    for layout, name in ((0, "rows"), (1, "vt_operand")):
+        def step():
+            _lib.check(lib.qmha_quantize_int8(X.data_ptr(), B, N, H * d, H, Xi.data_ptr(), sc.data_ptr(), layout, sptr),
+                       "quantize_int8")
+        for _ in range(3):
+            step()
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(steps):
+            step()
+        s1.record()
+        s1.synchronize()
+        ms = s0.elapsed_time(s1) / steps
+        nbytes = X.numel() * 4 + Xi.numel() + sc.numel() * 4
+        out[name] = {"ms": round(ms, 4), "GB_s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                     "roofline": {"bound": "hbm", "achieved": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+    out["config"] = f"one [{B}, {N}, {H * d}] fp32 tensor, {H} heads of d={d} (a C4 operand)"
+    out["algorithmic_bytes"] = X.numel() * 4 + Xi.numel() + sc.numel() * 4
+    return out
+
+
+def time_torch_ext(B, H, N, d, dev, steps=10):
+    """The reference's Python entry point (extensions/torch/torch_ext.cpp:11-58): the compiled
+    pybind `torch_ext.flash_solve(Q, K, V, d_model, num_heads, kernel)` -- one [N, d_model]
+    sequence per call, blocking, as the reference binds it -- B calls per step at the C4 shape,
+    beside the batched C-ABI call of the headline line (the binding's overhead)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "quantizedmha_amd", "lib"))
+    try:
+        import torch_ext  # the compiled pybind module (quantizedmha_amd/csrc/torch_ext.cpp)
+    finally:
+        sys.path.pop(0)
+    g = torch.Generator(device=dev).manual_seed(11)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+
+    def step():
+        for b in range(B):
+            torch_ext.flash_solve(Q[b], K[b], V[b], H * d, H, "fa_tc_int8_b")
+
+    step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    return {"pattern": f"{B} torch_ext.flash_solve calls (one [N, d_model] sequence each), kernel fa_tc_int8_b",
+            "module": getattr(torch_ext, "__file__", "?"), "ms_per_step": round(ms, 4),
+            "tflops": round(flops(B, H, N, d) / (ms * 1e-3) / 1e12, 3)}
 
 
 def reference_config(variant, dev, rank, world):

@@ -362,15 +362,11 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
         g_last_error = "bad scales pointer or layout";
         return QMHA_ERR_INVALID;
     }
-    // The pre-pass quantises Q, K, V in one launch; run it with X in the requested role and
-    // write only that role's output (the other two roles go to a scratch workspace).
-    const size_t need = qmha::int8_workspace_bytes(B, N, h, D);
-    void* ws = nullptr;
-    st = get_workspace(need, (hipStream_t)stream, &ws);
-    if (st != QMHA_OK) return st;
-    qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
-    void* vout = w.Vh;
-    int v_mode = 1;
+    // The pre-pass kernel with X in one role only: the Q role (row layout) or the V role (the
+    // V^T operand order); nothing else is written, no workspace is needed.
+    qmha::Int8Workspace w{};
+    void* vout = nullptr;
+    int v_mode = 1, role = 0;
     if (layout == 0) {
         w.Qi = Xi;
         w.sQ = scales;
@@ -378,8 +374,9 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
         vout = Xi;
         v_mode = 0;
         w.sV = scales;
+        role = 2;
     }
-    QMHA_HIP_TRY(qmha::launch_quant_int8(X, X, X, w, vout, v_mode, B, N, h, D, d_model, (hipStream_t)stream),
+    QMHA_HIP_TRY(qmha::launch_quant_int8(X, X, X, w, vout, v_mode, B, N, h, D, d_model, (hipStream_t)stream, role, 1),
                  "quant_int8 launch");
     return QMHA_OK;
 }

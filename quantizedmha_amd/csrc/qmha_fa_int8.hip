@@ -942,9 +942,10 @@ Int8Workspace int8_carve(void* ws, int B, int N, int H, int D) {
 
 template <int D>
 static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                               int v_mode, int B, int N, int H, int d_model, int first_tensor, hipStream_t stream) {
+                               int v_mode, int B, int N, int H, int d_model, int first_tensor, int num_tensors,
+                               hipStream_t stream) {
     const int total = B * H * (N / QMHA_GROUP);
-    dim3 grid((total + 3) / 4, 3 - first_tensor);
+    dim3 grid((total + 3) / 4, num_tensors > 0 ? num_tensors : 3 - first_tensor);
     if (v_mode == 0)
         hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 0>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
                            w.sK, w.sV, N, H, d_model, total, first_tensor);
@@ -955,11 +956,14 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
 }
 
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream, int first_tensor) {
+                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream, int first_tensor,
+                             int num_tensors) {
+    if (first_tensor < 0 || first_tensor > 2 || (num_tensors > 0 && first_tensor + num_tensors > 3))
+        return hipErrorInvalidValue;
     switch (D) {
-        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
-        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
-        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, stream);
+        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
         default: return hipErrorInvalidValue;
     }
 }

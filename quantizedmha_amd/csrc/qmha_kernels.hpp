@@ -26,10 +26,11 @@ struct Int8Workspace {
 size_t int8_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
-// first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V
+// first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V;
+// num_tensors (default: all from first_tensor on) limits the roles launched (the standalone op)
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
                              int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream,
-                             int first_tensor = 0);
+                             int first_tensor = 0, int num_tensors = -1);
 // Qf: the caller's fp32 Q (the main kernel quantises each Q group into its MFMA operand)
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream);
