@@ -14,6 +14,8 @@
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
+#include <type_traits>
+
 namespace qmha {
 
 static constexpr float kLog2eH = 1.4426950408889634f;
@@ -81,7 +83,9 @@ __device__ __forceinline__ int chunk_swz_h(int row) {
 // ---------------------------------------------------------------------------------------
 // F16_VPRE: the tile's V^T operands are read from LDS before its softmax, so the P@V MFMAs do
 // not wait on their LDS reads
-enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8 };
+// F16_UNROLL: two stages per loop trip, so each stage's LDS buffer is a compile-time constant and
+// every operand read is a base register plus an immediate (no per-tile address arithmetic)
+enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16 };
 
 template <int D, int WAVES, int SG, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f16_v2_kernel(
@@ -236,6 +240,28 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
 
     issue(0, 0);
     qmha_dma_barrier();
+    if constexpr (FL & F16_UNROLL) {
+        auto stage = [&](auto BUF, int st) {
+            constexpr int buf = decltype(BUF)::value;
+            if (st + 1 < nst) issue(buf ^ 1, st + 1);
+            if (active) {
+                const char* L = lds[buf];
+                const int ngr = G - st * SG;  // < SG only in a partial last stage (uniform)
+#pragma unroll
+                for (int gi = 0; gi < SG; ++gi) {
+                    if (gi == 0 || gi < ngr) tile(L, gi, qk(L, gi));
+                    __builtin_amdgcn_sched_barrier(0);  // one tile's registers at a time
+                }
+            }
+            qmha_dma_barrier();
+        };
+        int st = 0;
+        for (; st + 2 <= nst; st += 2) {
+            stage(std::integral_constant<int, 0>{}, st);
+            stage(std::integral_constant<int, 1>{}, st + 1);
+        }
+        if (st < nst) stage(std::integral_constant<int, 0>{}, st);
+    } else
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) issue(buf ^ 1, st + 1);
@@ -345,7 +371,7 @@ static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float
 }
 
 #ifndef QMHA_F16_FL
-#define QMHA_F16_FL (F16_LB4 | F16_VPRE)  // V operands before the softmax: -1.7 % (profiles/r02/ab/f16_vpre)
+#define QMHA_F16_FL (F16_LB4 | F16_VPRE | F16_UNROLL)  // V operands before the softmax: -1.7 % (profiles/r02/ab/f16_vpre)
 #endif
 template <int D>
 static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
