@@ -67,7 +67,8 @@ def header_deps():
 # -fno-honor-nans: fmaxf on MFMA results and running maxima otherwise gets a canonicalising
 # v_max (x, x) in front of it (5 per fp16 tile; scores here are finite by construction)
 FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize", "-fno-honor-nans"] + os.environ.get("QMHA_INT8_FLAGS", "").split(),
-              "qmha_fa_f16.hip": ["-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split()}
+              "qmha_fa_f16.hip": ["-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split(),
+              "qmha_fa_f32.hip": os.environ.get("QMHA_F32_FLAGS", "").split()}
 
 
 def compile_one(src, extra=()):
