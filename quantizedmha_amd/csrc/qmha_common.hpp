@@ -238,3 +238,33 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
         *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
     }
 }
+
+// The same for the int8 V^T operand ([D][32 slots] bytes, kv_of_slot_i8 order; the standalone
+// qmha_quantize_int8 layout 1): four consecutive kv rows are four consecutive slots, so a lane
+// packs its 4-row runs of one column into one dword (ds_write_b32 instead of byte stores).
+constexpr int QMHA_VT8_PITCH = 32 + 4;  // bytes per d-row of the int8 LDS tile
+template <int D>
+__device__ __forceinline__ void vt8_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
+    constexpr int C4 = D / 4, NI = D / 8;
+    const int rq = lane / C4, c4 = lane % C4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int d = 4 * c4 + c;
+#pragma unroll
+        for (int a = 0; a < NI / 4; ++a) {  // kv rows NI rq + 4a .. +3 -> 4 consecutive slots
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w |= ((uint32_t)(uint8_t)qmha_quant_i8(x[4 * a + e][c], inv)) << (8 * e);
+            *reinterpret_cast<uint32_t*>(T + d * QMHA_VT8_PITCH + slot_of_kv_i8(NI * rq + 4 * a)) = w;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    constexpr int LINES = D * 32 / 16;  // 16-byte output lines of the group
+#pragma unroll
+    for (int u = lane; u < LINES; u += 64) {
+        const int d = u >> 1, q = u & 1;
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(T + d * QMHA_VT8_PITCH + 16 * q);
+        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{(int)r[0], (int)r[1], (int)r[2], (int)r[3]};
+    }
+}

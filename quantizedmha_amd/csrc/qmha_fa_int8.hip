@@ -73,9 +73,9 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const int b = bh / H, k = bh % H;
     const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
 
-    if (tensor == 2 && v_mode == 1) {
-        // V into the f16 V^T operand order ([d][32 slots] f16 per group) through a per-wave LDS
-        // transpose: coalesced 16-byte loads (instruction i covers rows i, NI+i, ...: 256-byte row
+    if (tensor == 2) {
+        // V into the V^T operand order ([d][32 slots] per group: f16 integers for the attention
+        // path, int8 for the standalone op) through a per-wave LDS transpose: coalesced 16-byte loads (instruction i covers rows i, NI+i, ...: 256-byte row
         // segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns 4 c4..4 c4+3.  In the
         // slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots (kv_of_slot_f16), so
         // each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile is read back
@@ -98,8 +98,11 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
         const float sc = qmha_scale_from_absmax(amax);
         const float inv = 1.0f / sc;
         if (active) {
-            vt_group_store<D, true>(vtr[wave], x, inv, lane,
-                                    static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
+            if constexpr (v_mode == 1)
+                vt_group_store<D, true>(vtr[wave], x, inv, lane,
+                                        static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
+            else
+                vt8_group_store<D>(vtr[wave], x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
             if (lane == 0) sV[item] = sc;
         }
         return;
@@ -132,28 +135,6 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
                 *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
             }
             if (lane == 0) (tensor == 0 ? sQ : sK)[item] = sc;
-        }
-    } else if constexpr (v_mode == 0) {
-        // int8 [D][32] with the i8 operand slot permutation, transposed through LDS (only for
-        // the standalone qmha_quantize_int8 op; the attention path uses VMODE 1 above)
-        __shared__ __attribute__((aligned(16))) int8_t vtile[4][32 * D];
-        int8_t* tile = vtile[wave];
-        if (active) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int slot = slot_of_kv_i8(i * RPI + ri);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) tile[(4 * ci + c) * 32 + slot] = (int8_t)qmha_quant_i8(v[i][c], inv);
-            }
-        }
-        qmha_dma_barrier();
-        if (active) {
-            int8_t* dst = static_cast<int8_t*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D);
-            constexpr int CH = 32 * D / 16;
-#pragma unroll
-            for (int c = lane; c < CH; c += 64)
-                reinterpret_cast<v4i*>(dst)[c] = reinterpret_cast<const v4i*>(tile)[c];
-            if (lane == 0) sV[item] = sc;
         }
     }
 }
