@@ -1027,6 +1027,11 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9049: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY | FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
             case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
             case 9043: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
+            // workgroup size: each LDS-DMA stage shared by more waves (fewer pieces per wave)
+            case 9061: return fa_int8_pipe_launch<D, 6, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9081: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9121: return fa_int8_pipe_launch<D, 12, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9021: return fa_int8_pipe_launch<D, 2, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
