@@ -257,6 +257,20 @@ def pmc_traffic(variant, B, H, N, d):
     return None, None
 
 
+def pmc_sq(variant, B, H, N, d):
+    """MFMA-busy % of the main kernel from the committed SQ counter passes
+    (profiles/*/pmc_sq_<variant>.json, tools/pmc_sq.sh): the rocprofv3 cross-check SURVEY 8(d) asks for."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_sq_{variant}.json")), reverse=True):
+        try:
+            j = json.load(open(path))
+            if j.get("shape") == [B, H, N, d]:
+                return j.get("mfma_busy_pct"), os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
 def spawn_ranks(n):
     """`--gpus N` (N > 1) outside a torch.distributed launcher: start the N rank processes (one
     per GPU, rendezvous on 127.0.0.1) with torch.distributed.run as a CHILD process and return
@@ -360,6 +374,7 @@ def main():
     peak = PEAKS.get(a.variant, INT8_PEAK_TOPS)
     achieved = flops(B, H, N, d) / (r["main_kernel_ms"] * 1e-3) / 1e12 if r["main_kernel_ms"] > 0 else 0.0
     traffic, traffic_src = pmc_traffic(a.variant, B, H, N, d)
+    busy, busy_src = pmc_sq(a.variant, B, H, N, d)
     hbm_alg = 16.0 * B * N * H * d  # fp32 Q, K, V read once + O written once (per call)
     res = {
         "metric": "attention-fwd TFLOPS + ms/call, B16 H16 N4096 d64 (fp16 & int8)",
@@ -391,7 +406,9 @@ def main():
                            "algorithmic_flops_per_launch": flops(B, H, N, d),
                            "main_kernel_ms": round(r["main_kernel_ms"], 4),
                            "prepass_ms": round(r["prepass_ms"], 4),
-                           "hbm_algorithmic_bytes_per_call": hbm_alg}
+                           "hbm_algorithmic_bytes_per_call": hbm_alg,
+                           "hbm_GBs_per_call": round(hbm_alg / (r["ms_per_step"] * 1e-3) / 1e9, 1),
+                           "mfma_busy_pct": busy, "mfma_busy_source": busy_src}
     if dist.is_initialized():
         ag_ms = time_allgather(r["O"], max(3, a.steps // 2), dev, world)
         sg_ms = time_solve_gather(a.variant, r["inputs"], H, d, max(3, a.steps // 2), dev, world,
