@@ -18,7 +18,7 @@ def main():
     win = d[skip:skip + count]
     print(f"{pat}: {len(d)} dispatches, average {sum(d) / len(d):.4f} ms; "
           f"dispatches {skip}..{skip + len(win) - 1} (bench's timed window) average {sum(win) / max(1, len(win)):.4f} ms, "
-          f"min {min(d):.4f}, max {max(d):.4f}")
+          f"window min {min(win):.4f}, max {max(win):.4f} (all dispatches: min {min(d):.4f}, max {max(d):.4f})")
 
 
 if __name__ == "__main__":
