@@ -52,91 +52,102 @@ static constexpr float kLog2e = 1.4426950408889634f;
 // v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
 // v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
 // ---------------------------------------------------------------------------------------
+// One wave quantises one 32-row group of V (b, k, g) into the V^T operand order through its
+// LDS tile `vtr` (D * QMHA_VT_PITCH bytes): coalesced 16-byte loads (instruction i covers rows
+// i, NI+i, ...: 256-byte row segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns
+// 4 c4..4 c4+3.  In the slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots
+// (kv_of_slot_f16), so each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile
+// is read back in 8-byte pieces and stored as 16-byte lines.  Loads are non-temporal: fp32
+// K/V are read exactly once per call.
+// v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
+// v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
+template <int D, int VMODE>
+__device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void* __restrict__ Vout,
+                                              float* __restrict__ sV, char* vtr, int lane, int b, int k, int g,
+                                              int bh, int N, int G, int d_model) {
+    constexpr int C4 = D / 4, NI = 32 / (64 / C4);
+    const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
+    v4f x[NI];
+    float amax = 0.0f;
+    const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
+    }
+    amax = wave_max64(amax);
+    const float sc = qmha_scale_from_absmax(amax);
+    const float inv = 1.0f / sc;
+    if constexpr (VMODE == 1)
+        vt_group_store<D, true>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
+    else
+        vt8_group_store<D>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
+    if (lane == 0) sV[(size_t)bh * G + g] = sc;
+}
+
+// One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
+template <int D>
+__device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int8_t* __restrict__ Xi,
+                                                float* __restrict__ sX, int lane, int b, int k, int g, int bh, int N,
+                                                int G, int d_model) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
+    const int ri = lane / C4, ci = lane % C4;
+    v4f v[NI];
+    float amax = 0.0f;
+    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        v[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
+    }
+    amax = wave_max64(amax);
+    const float sc = qmha_scale_from_absmax(amax);  // :104
+    const float inv = 1.0f / sc;                     // :106 (correctly rounded division)
+    int8_t* dst = Xi + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
+        *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
+    }
+    if (lane == 0) sX[(size_t)bh * G + g] = sc;
+}
+
+// ---------------------------------------------------------------------------------------
+// Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
+// One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
+// sel_delta > 0 (the fused int8 path, qmha_fa_int8_pipe_kernel FL_FUSE): only the first
+// sel_delta heads of every run of sel_hpx heads (the heads no main-kernel workgroup produces),
+// and the per-head ready counters cnt[0, nheads) are zeroed for the main kernel.
+// ---------------------------------------------------------------------------------------
 template <int D, int VMODE>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int first_tensor) {
-    constexpr int v_mode = VMODE;
-    constexpr int C4 = D / 4;        // float4 per row
-    constexpr int RPI = 64 / C4;     // rows per load instruction
-    constexpr int NI = 32 / RPI;     // load instructions per lane
-
+    int N, int H, int d_model, int total_groups, int first_tensor,
+    int sel_delta = 0, int sel_hpx = 0, int* __restrict__ cnt = nullptr, int nheads = 0) {
+    __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
     const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    if (cnt && blockIdx.y == 0)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < nheads; i += gridDim.x * 256) cnt[i] = 0;
     const int item = blockIdx.x * 4 + wave;  // (bh, g)
-    const bool active = item < total_groups;
+    if (item >= total_groups) return;        // wave-uniform
     const int G = N / QMHA_GROUP;
-    const int bh = active ? item / G : 0, g = active ? item % G : 0;
+    int bh = item / G;
+    const int g = item % G;
+    if (sel_delta > 0) bh = (bh / sel_delta) * sel_hpx + bh % sel_delta;
     const int b = bh / H, k = bh % H;
-    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
-
-    if (tensor == 2) {
-        // V into the V^T operand order ([d][32 slots] per group: f16 integers for the attention
-        // path, int8 for the standalone op) through a per-wave LDS transpose: coalesced 16-byte loads (instruction i covers rows i, NI+i, ...: 256-byte row
-        // segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns 4 c4..4 c4+3.  In the
-        // slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots (kv_of_slot_f16), so
-        // each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile is read back
-        // in 8-byte pieces and stored as 16-byte lines.  Loads are non-temporal: fp32 K/V are
-        // read exactly once per call.
-        __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
-        const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
-        v4f x[NI];
-        float amax = 0.0f;
-        if (active) {
-            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
-#pragma unroll
-                for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
-            }
-        }
-        amax = wave_max64(amax);
-        const float sc = qmha_scale_from_absmax(amax);
-        const float inv = 1.0f / sc;
-        if (active) {
-            if constexpr (v_mode == 1)
-                vt_group_store<D, true>(vtr[wave], x, inv, lane,
-                                        static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
-            else
-                vt8_group_store<D>(vtr[wave], x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
-            if (lane == 0) sV[item] = sc;
-        }
-        return;
-    }
-
-    const int ri = lane / C4, ci = lane % C4;
-    v4f v[NI];
-    float amax = 0.0f;
-    if (active) {
-        const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            v[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
-#pragma unroll
-            for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
-        }
-    }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);  // :104
-    const float inv = 1.0f / sc;                     // :106 (correctly rounded division)
-
-    if (tensor < 2) {
-        if (active) {
-            int8_t* dst = (tensor == 0 ? Qi : Ki) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
-                *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
-            }
-            if (lane == 0) (tensor == 0 ? sQ : sK)[item] = sc;
-        }
-    }
+    if (tensor == 2)
+        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
+    else
+        quant_row_group<D>(tensor == 0 ? Q : K, tensor == 0 ? Qi : Ki, tensor == 0 ? sQ : sK, lane, b, k, g, bh, N, G,
+                           d_model);
 }
 
 // LDS XOR swizzle for a row of RB bytes read as 16-byte chunks by ds_read_b128 with one
@@ -209,7 +220,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //               tile (bias removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump:
 //               the bit-exact check of the production Q@K^T path; never the production launch)
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
-       FL_DUMP = 256 };
+       FL_DUMP = 256, FL_PIN = 512, FL_FUSE = 1024 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -482,11 +493,27 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
+}
+
+#ifndef QMHA_FUSE_RELEASE
+#define QMHA_FUSE_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#endif
+#ifndef QMHA_FUSE_ACQUIRE
+#define QMHA_FUSE_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#endif
+#ifndef QMHA_PIPE_ATTR  // profiling builds may cap the register budget, e.g. amdgpu_num_vgpr
+#define QMHA_PIPE_ATTR
+#endif
 template <int D, int WAVES, int FL, int PAD = 0>
-__global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
+__global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg, FuseArgs fz) {
     constexpr int SG = 2, RING = 3;
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
@@ -506,6 +533,48 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     const int qg = qb * WAVES + wave;
     const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
 
+    if constexpr (FL & FL_FUSE) {
+        // (1) produce this workgroup's share of head bh + delta (the same XCD run of heads: the
+        // launcher requires nwg % 8 == 0 and whole heads per run, so the run is blockIdx % 8 and
+        // bh = run * hpx + hr): wave w quantises K group 4 j + w and V group 4 j + w, exactly as
+        // the pre-pass does.  Head bh + delta's workgroups start about delta head-generations
+        // later on this XCD, by when the share is long written.
+        static_assert(WAVES == 4 && WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "fused producer geometry");
+        const int o = blockIdx.x >> 3, hr = o / nqb, j = o % nqb;
+        char* vtr = reinterpret_cast<char*>(&lds[0][0]) + wave * D * QMHA_VT_PITCH;
+        if (fz.produce && hr + fz.delta < fz.hpx) {
+            const int bhp = bh + fz.delta, g = 4 * j + wave;
+            if (g < G) {
+                quant_row_group<D>(fz.Kf, fz.Ki, fz.sK, lane, bhp / H, bhp % H, g, bhp, N, G, d_model);
+                quant_v_group<D, 1>(fz.Vf, fz.Vh, fz.sV, vtr, lane, bhp / H, bhp % H, g, bhp, N, G, d_model);
+            }
+            QMHA_FUSE_RELEASE();  // this wave's K/V stores before the count
+            __syncthreads();
+            if (threadIdx.x == 0) atomicAdd(fz.cnt + bhp, 1);
+        }
+        // (2) this head's K/V: heads hr < delta came from the pre-launch (stream order); the
+        // rest wait for their nqb producer workgroups, bounded -- past the bound the workgroup
+        // quantises the whole head itself (identical bytes, so a late producer's stores are
+        // harmless), so no dispatch order can deadlock the grid
+        if (hr >= fz.delta) {
+            __shared__ int ready;
+            if (threadIdx.x == 0) {
+                int it = 0;
+                while (__hip_atomic_load(fz.cnt + bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nqb && ++it < 4096)
+                    __builtin_amdgcn_s_sleep(4);
+                ready = it < 4096;
+            }
+            __syncthreads();
+            if (!ready) {
+                for (int g = wave; g < G; g += WAVES) {
+                    quant_row_group<D>(fz.Kf, fz.Ki, fz.sK, lane, b, k, g, bh, N, G, d_model);
+                    quant_v_group<D, 1>(fz.Vf, fz.Vh, fz.sV, vtr, lane, b, k, g, bh, N, G, d_model);
+                }
+            }
+            QMHA_FUSE_ACQUIRE();  // the producers' (or this workgroup's own) stores
+        }
+        __syncthreads();  // every wave is done with its LDS scratch before the ring fills
+    }
     v4i qop[D / 32];
     float cq = 0.0f;
     constexpr bool DUMP = FL & FL_DUMP;
@@ -630,6 +699,11 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // row's 1/sP and its row-sum scale, because the P tile's one scale sP is shared by rows with
     // different f.  Saves the 16 bias subtractions per tile for 4 per-row operations.
     constexpr bool KFOLD = MAGIC && (FL & FL_KFOLD);
+    // FL_PIN: each softmax chunk's results pass through an empty volatile asm at the chunk's end,
+    // so IR-level code motion cannot sink the chunk past the sched_barrier fences (without it the
+    // P quantisation sinks into the next iteration and whole chunks cross the stage barrier,
+    // leaving runs of back-to-back MFMAs with no VALU between them)
+    constexpr bool PIN = FL & FL_PIN;
     // FL_EARLY: the serial head of a tile (row max -> running max -> P-tile max -> sP -> 1/sP)
     // runs at the end of the previous iteration, in one scheduling region with that
     // iteration's O update, so its latency chain interleaves with independent work
@@ -764,6 +838,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 x[r] = fmaf(sv, c, -m_new);
             }
         }
+        if constexpr (PIN) pin_regs(x, 0, 8);
         QMHA_FENCE();
         mfmas(1);
         QMHA_FENCE();
@@ -777,6 +852,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 x[r] = fmaf(sv, c, -m_new);
             }
         }
+        if constexpr (PIN) pin_regs(x, 8, 16);
         QMHA_FENCE();
         mfmas(2);
         QMHA_FENCE();
@@ -784,12 +860,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         float p[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        if constexpr (PIN) pin_regs(p, 0, 8);
         QMHA_FENCE();
         mfmas(3);
         QMHA_FENCE();
         // ---- E: p = exp2, rows 8..15
 #pragma unroll
         for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        if constexpr (PIN) pin_regs(p, 8, 16);
         QMHA_FENCE();
         mfmas(4);
         QMHA_FENCE();
@@ -804,6 +882,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
             pc[r >> 2][2 * (r & 3)] = h2[0];
             pc[r >> 2][2 * (r & 3) + 1] = h2[1];
+        }
+        if constexpr (PIN) {
+            asm volatile("" : "+v"(pc[0]));
+            asm volatile("" : "+v"(pc[1]));
         }
         QMHA_FENCE();
         mfmas(5);
@@ -963,7 +1045,7 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
 
 template <int D, int WAVES, int FL, int PAD = 0>
 static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
-                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}) {
+                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}, FuseArgs fz = FuseArgs{}) {
     const int G = N / QMHA_GROUP;
     if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
@@ -975,7 +1057,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     constexpr int lds_pad = 0;
 #endif
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, fz);
     return hipGetLastError();
 }
 
@@ -1041,6 +1123,43 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     }
     if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
     return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
+}
+
+// fused path: main-kernel workgroups of head h produce head h + delta of their XCD run
+#ifndef QMHA_FUSE_DELTA
+#define QMHA_FUSE_DELTA 3
+#endif
+
+bool fa_int8_fused_plan(int B, int N, int H, int D, int* hpx, int* delta) {
+    const int G = N / QMHA_GROUP, nqb = (G + 3) / 4, nwg = B * H * nqb;
+#ifdef QMHA_ABLATION
+    static const int dl = std::getenv("QMHA_FUSE_DELTA") ? std::atoi(std::getenv("QMHA_FUSE_DELTA")) : QMHA_FUSE_DELTA;
+#else
+    constexpr int dl = QMHA_FUSE_DELTA;
+#endif
+    // whole heads per XCD run (nwg % 8 == 0, run length a multiple of nqb), more heads per run
+    // than the pre-launch covers, and per-head scale arrays on whole 64-byte lines (G % 16 == 0:
+    // no scalar-cache line is shared with a head produced later)
+    if (D != 64 || G < 2 || dl < 1 || nwg % 8 != 0 || (nwg / 8) % nqb != 0 || G % 16 != 0) return false;
+    *hpx = nwg / 8 / nqb;
+    *delta = dl;
+    return *hpx > dl;
+}
+
+hipError_t launch_fa_int8_fused_pre(const Int8Workspace& w, int* cnt, const float* Kf, const float* Vf, int B, int N,
+                                    int H, int d_model, int hpx, int delta, hipStream_t stream) {
+    const int pre_groups = 8 * delta * (N / QMHA_GROUP);
+    hipLaunchKernelGGL((qmha_quant_int8_kernel<64, 1>), dim3((pre_groups + 3) / 4, 2), dim3(256), 0, stream, nullptr, Kf,
+                       Vf, nullptr, w.Ki, (void*)w.Vh, nullptr, w.sK, w.sV, N, H, d_model, pre_groups, 1, delta, hpx,
+                       cnt, B * H);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_int8_fused_main(const Int8Workspace& w, int* cnt, const float* Qf, const float* Kf,
+                                     const float* Vf, float* O, int B, int N, int H, int d_model, int hpx, int delta,
+                                     int produce, hipStream_t stream) {
+    const FuseArgs fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, cnt, hpx, delta, produce};
+    return fa_int8_pipe_launch<64, 4, kD64Flags | FL_FUSE>(w, Qf, O, B, N, H, d_model, stream, QkDump{}, fz);
 }
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
