@@ -308,9 +308,6 @@ def main():
                     help="skip the reference's own configuration (include/config.h: N8192 d_model1024 h32)")
     ap.add_argument("--gather-chunks", type=int, default=4,
                     help="batch chunks of the compute+all-gather step (gather of chunk c overlaps chunk c+1)")
-    ap.add_argument("--int8-fused", type=int, default=0, choices=(0, 1, 2),
-                    help="int8 path: 1 = main-kernel workgroups quantise later heads' K/V (qmha_set_int8_fused), "
-                         "0 = separate pre-pass launch for all heads")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher plumbing only (CPU, gloo): spawn, rendezvous, barriers, max-over-ranks "
                          "timing and the chunked all-gather, with a tensor copy as the step; no kernel, no value")
@@ -321,8 +318,6 @@ def main():
         sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if not a.dry_run:
-        _lib.load().qmha_set_int8_fused(a.int8_fused)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         sys.stderr.write(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks\n")
@@ -397,7 +392,7 @@ def main():
                  "synthetic N(0, 0.5^2) fp32 Q/K/V, torch.Generator seed 1234+rank, resident in HBM"),
         "config": {"workload": f"{a.variant} attention forward (BASELINE config {'5' if world > 1 else '4'})",
                    "variant": a.variant, "B_per_gpu": B, "H": H, "N": N, "d": d, "d_model": H * d,
-                   "global_batch": B * world, "int8_fused": a.int8_fused,
+                   "global_batch": B * world,
                    "parallelism": f"batch-shard x{world} (no collective in the timed step; all-gather reported "
                                   f"separately)"},
     }

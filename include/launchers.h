@@ -128,13 +128,6 @@ void qmha_profile_enable(int on);
 /* Number of batch chunks for the pre-pass / main-kernel overlap (1..16, 1 = off); returns the
  * previous value.  Results are bit-identical for every setting. */
 int qmha_set_overlap_chunks(int n);
-/* Fused int8 path (mode 1, the default; used when the overlap is off and the shape qualifies:
- * d = 64, whole heads per XCD run of workgroups): the main kernel's workgroups quantise the K/V
- * of a later head while earlier heads compute, so only the first heads' K/V pass through a
- * separate pre-pass launch.  0 = the two-launch path; 2 = fused with the in-kernel producers
- * skipped, so every later head takes the bounded-wait fallback (a test hook).  Returns the
- * previous mode.  Results are bit-identical in every mode. */
-int qmha_set_int8_fused(int mode);
 int qmha_profile_collect(double *main_ms, long long *launches, double *prepass_ms);
 
 /* Release all library-owned workspaces (optional; also released at process exit). */

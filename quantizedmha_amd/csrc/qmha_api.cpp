@@ -107,7 +107,6 @@ struct SideStream {
 std::mutex g_side_mu;
 std::map<std::pair<int, void*>, SideStream> g_side;
 
-std::atomic<int> g_int8_fused{0};  // qmha_set_int8_fused: 0 off, 1 on, 2 on without producers (test hook)
 std::atomic<int> g_overlap_chunks{-1};  // -1: not yet read from QMHA_OVERLAP_CHUNKS
 
 int overlap_chunks(int B) {
@@ -249,28 +248,6 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
         }
         const hipStream_t pre_s = nc > 1 ? side->s : stream;
         const qmha::Int8Workspace w8 = variant == QMHA_FA_TC_INT8_B ? qmha::int8_carve(ws, B, N, h, D) : qmha::Int8Workspace{};
-        int hpx = 0, delta = 0;
-        const int fmode = g_int8_fused.load();
-        if (variant == QMHA_FA_TC_INT8_B && nc == 1 && fmode != 0 && qmha::fa_int8_fused_plan(B, N, h, D, &hpx, &delta)) {
-            // one pre-launch for the first heads of every XCD run, then the main kernel whose
-            // workgroups quantise the later heads' K/V (the solve path never uses the Qi region:
-            // it holds the per-head ready counters)
-            int* cnt = reinterpret_cast<int*>(w8.Qi);
-            QMHA_MARK(rec.pre, stream, true);
-            QMHA_HIP_TRY(qmha::launch_fa_int8_fused_pre(w8, cnt, K, V, B, N, h, d_model, hpx, delta, stream),
-                         "quant_int8 pre-launch");
-            QMHA_MARK(rec.pre, stream, false);
-            QMHA_MARK(rec.main, stream, true);
-            QMHA_HIP_TRY(qmha::launch_fa_int8_fused_main(w8, cnt, Q, K, V, O, B, N, h, d_model, hpx, delta,
-                                                         fmode == 1, stream),
-                         "fa_int8 fused launch");
-            QMHA_MARK(rec.main, stream, false);
-            if (prof) {
-                std::lock_guard<std::mutex> lk(g_prof_mu);
-                g_prof_recs.push_back(std::move(rec));
-            }
-            return QMHA_OK;
-        }
         const qmha::F16Workspace w16 = variant == QMHA_FA_TC_V1A ? qmha::f16_carve(ws, B, N, h, D) : qmha::F16Workspace{};
         // every pre-pass is enqueued first (the side stream runs ahead), then the main kernels
         for (int c = 0; c < nc; ++c) {
@@ -478,8 +455,6 @@ const char* qmha_status_string(int s) {
 const char* qmha_version(void) { return QMHA_VERSION_STRING; }
 
 const char* qmha_last_error(void) { return g_last_error.c_str(); }
-
-int qmha_set_int8_fused(int mode) { return g_int8_fused.exchange(mode < 0 ? 0 : (mode > 2 ? 2 : mode)); }
 
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);

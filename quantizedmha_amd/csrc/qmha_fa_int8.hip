@@ -119,29 +119,21 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
 // ---------------------------------------------------------------------------------------
 // Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
 // One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
-// sel_delta > 0 (the fused int8 path, qmha_fa_int8_pipe_kernel FL_FUSE): only the first
-// sel_delta heads of every run of sel_hpx heads (the heads no main-kernel workgroup produces),
-// and the per-head ready counters cnt[0, nheads) are zeroed for the main kernel.
 // ---------------------------------------------------------------------------------------
 template <int D, int VMODE>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int first_tensor,
-    int sel_delta = 0, int sel_hpx = 0, int* __restrict__ cnt = nullptr, int nheads = 0) {
+    int N, int H, int d_model, int total_groups, int first_tensor) {
     __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
     const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    if (cnt && blockIdx.y == 0)
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < nheads; i += gridDim.x * 256) cnt[i] = 0;
     const int item = blockIdx.x * 4 + wave;  // (bh, g)
     if (item >= total_groups) return;        // wave-uniform
     const int G = N / QMHA_GROUP;
-    int bh = item / G;
-    const int g = item % G;
-    if (sel_delta > 0) bh = (bh / sel_delta) * sel_hpx + bh % sel_delta;
+    const int bh = item / G, g = item % G;
     const int b = bh / H, k = bh % H;
     if (tensor == 2)
         quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
@@ -220,7 +212,8 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //               tile (bias removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump:
 //               the bit-exact check of the production Q@K^T path; never the production launch)
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
-       FL_DUMP = 256, FL_PIN = 512, FL_FUSE = 1024 };
+       FL_DUMP = 256, FL_PIN = 512,
+       FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -500,12 +493,6 @@ __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
         if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
 }
 
-#ifndef QMHA_FUSE_RELEASE
-#define QMHA_FUSE_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
-#endif
-#ifndef QMHA_FUSE_ACQUIRE
-#define QMHA_FUSE_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
-#endif
 #ifndef QMHA_PIPE_ATTR  // profiling builds may cap the register budget, e.g. amdgpu_num_vgpr
 #define QMHA_PIPE_ATTR
 #endif
@@ -513,7 +500,7 @@ template <int D, int WAVES, int FL, int PAD = 0>
 __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg, FuseArgs fz) {
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
     constexpr int SG = 2, RING = 3;
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
@@ -533,48 +520,6 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     const int qg = qb * WAVES + wave;
     const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
 
-    if constexpr (FL & FL_FUSE) {
-        // (1) produce this workgroup's share of head bh + delta (the same XCD run of heads: the
-        // launcher requires nwg % 8 == 0 and whole heads per run, so the run is blockIdx % 8 and
-        // bh = run * hpx + hr): wave w quantises K group 4 j + w and V group 4 j + w, exactly as
-        // the pre-pass does.  Head bh + delta's workgroups start about delta head-generations
-        // later on this XCD, by when the share is long written.
-        static_assert(WAVES == 4 && WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "fused producer geometry");
-        const int o = blockIdx.x >> 3, hr = o / nqb, j = o % nqb;
-        char* vtr = reinterpret_cast<char*>(&lds[0][0]) + wave * D * QMHA_VT_PITCH;
-        if (fz.produce && hr + fz.delta < fz.hpx) {
-            const int bhp = bh + fz.delta, g = 4 * j + wave;
-            if (g < G) {
-                quant_row_group<D>(fz.Kf, fz.Ki, fz.sK, lane, bhp / H, bhp % H, g, bhp, N, G, d_model);
-                quant_v_group<D, 1>(fz.Vf, fz.Vh, fz.sV, vtr, lane, bhp / H, bhp % H, g, bhp, N, G, d_model);
-            }
-            QMHA_FUSE_RELEASE();  // this wave's K/V stores before the count
-            __syncthreads();
-            if (threadIdx.x == 0) atomicAdd(fz.cnt + bhp, 1);
-        }
-        // (2) this head's K/V: heads hr < delta came from the pre-launch (stream order); the
-        // rest wait for their nqb producer workgroups, bounded -- past the bound the workgroup
-        // quantises the whole head itself (identical bytes, so a late producer's stores are
-        // harmless), so no dispatch order can deadlock the grid
-        if (hr >= fz.delta) {
-            __shared__ int ready;
-            if (threadIdx.x == 0) {
-                int it = 0;
-                while (__hip_atomic_load(fz.cnt + bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nqb && ++it < 4096)
-                    __builtin_amdgcn_s_sleep(4);
-                ready = it < 4096;
-            }
-            __syncthreads();
-            if (!ready) {
-                for (int g = wave; g < G; g += WAVES) {
-                    quant_row_group<D>(fz.Kf, fz.Ki, fz.sK, lane, b, k, g, bh, N, G, d_model);
-                    quant_v_group<D, 1>(fz.Vf, fz.Vh, fz.sV, vtr, lane, b, k, g, bh, N, G, d_model);
-                }
-            }
-            QMHA_FUSE_ACQUIRE();  // the producers' (or this workgroup's own) stores
-        }
-        __syncthreads();  // every wave is done with its LDS scratch before the ring fills
-    }
     v4i qop[D / 32];
     float cq = 0.0f;
     constexpr bool DUMP = FL & FL_DUMP;
@@ -682,8 +627,17 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
+    // FL_ABL_NOMFMA / FL_ABL_NOEXP (timing perturbations, QMHA_ABLATION builds only; results are
+    // wrong): every MFMA / every exp of the softmax replaced by an empty asm that keeps its
+    // operands and result live, so the rest of the loop compiles to the same VALU work
+    constexpr bool NOMFMA = FL & FL_ABL_NOMFMA, NOEXP = FL & FL_ABL_NOEXP;
     auto qk = [&](const v4i& kk, int ks) {
-        s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
+        if constexpr (NOMFMA) {
+            if (ks == 0) s_nxt = magic_blk;
+            asm volatile("" : "+v"(s_nxt) : "v"(kk), "v"(qop[ks]));
+        } else {
+            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
+        }
     };
     v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
     float scale_prev = 0.0f;
@@ -799,9 +753,15 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                         if (has_next) qk(JIT ? kop(ks) : kk[ks], ks);
                     } else {
                         const int m = op >> 1, ks = op & 1;
-                        if (has_prev)
-                            a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
-                                                                          ks == 0 ? v16f{} : a[m], 0, 0, 0);
+                        if (has_prev) {
+                            if constexpr (NOMFMA) {
+                                if (ks == 0) a[m] = v16f{};
+                                asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                            } else {
+                                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                              ks == 0 ? v16f{} : a[m], 0, 0, 0);
+                            }
+                        }
                     }
                 }
             }
@@ -859,14 +819,28 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         // ---- D: p = exp2, rows 0..7
         float p[16];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        for (int r = 0; r < 8; ++r) {
+            if constexpr (NOEXP) {
+                p[r] = x[r];
+                asm volatile("" : "+v"(p[r]));
+            } else {
+                p[r] = __builtin_amdgcn_exp2f(x[r]);
+            }
+        }
         if constexpr (PIN) pin_regs(p, 0, 8);
         QMHA_FENCE();
         mfmas(3);
         QMHA_FENCE();
         // ---- E: p = exp2, rows 8..15
 #pragma unroll
-        for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        for (int r = 8; r < 16; ++r) {
+            if constexpr (NOEXP) {
+                p[r] = x[r];
+                asm volatile("" : "+v"(p[r]));
+            } else {
+                p[r] = __builtin_amdgcn_exp2f(x[r]);
+            }
+        }
         if constexpr (PIN) pin_regs(p, 8, 16);
         QMHA_FENCE();
         mfmas(4);
@@ -1045,7 +1019,7 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
 
 template <int D, int WAVES, int FL, int PAD = 0>
 static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
-                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}, FuseArgs fz = FuseArgs{}) {
+                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}) {
     const int G = N / QMHA_GROUP;
     if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
@@ -1057,7 +1031,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     constexpr int lds_pad = 0;
 #endif
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, fz);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
     return hipGetLastError();
 }
 
@@ -1123,43 +1097,6 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     }
     if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
     return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
-}
-
-// fused path: main-kernel workgroups of head h produce head h + delta of their XCD run
-#ifndef QMHA_FUSE_DELTA
-#define QMHA_FUSE_DELTA 3
-#endif
-
-bool fa_int8_fused_plan(int B, int N, int H, int D, int* hpx, int* delta) {
-    const int G = N / QMHA_GROUP, nqb = (G + 3) / 4, nwg = B * H * nqb;
-#ifdef QMHA_ABLATION
-    static const int dl = std::getenv("QMHA_FUSE_DELTA") ? std::atoi(std::getenv("QMHA_FUSE_DELTA")) : QMHA_FUSE_DELTA;
-#else
-    constexpr int dl = QMHA_FUSE_DELTA;
-#endif
-    // whole heads per XCD run (nwg % 8 == 0, run length a multiple of nqb), more heads per run
-    // than the pre-launch covers, and per-head scale arrays on whole 64-byte lines (G % 16 == 0:
-    // no scalar-cache line is shared with a head produced later)
-    if (D != 64 || G < 2 || dl < 1 || nwg % 8 != 0 || (nwg / 8) % nqb != 0 || G % 16 != 0) return false;
-    *hpx = nwg / 8 / nqb;
-    *delta = dl;
-    return *hpx > dl;
-}
-
-hipError_t launch_fa_int8_fused_pre(const Int8Workspace& w, int* cnt, const float* Kf, const float* Vf, int B, int N,
-                                    int H, int d_model, int hpx, int delta, hipStream_t stream) {
-    const int pre_groups = 8 * delta * (N / QMHA_GROUP);
-    hipLaunchKernelGGL((qmha_quant_int8_kernel<64, 1>), dim3((pre_groups + 3) / 4, 2), dim3(256), 0, stream, nullptr, Kf,
-                       Vf, nullptr, w.Ki, (void*)w.Vh, nullptr, w.sK, w.sV, N, H, d_model, pre_groups, 1, delta, hpx,
-                       cnt, B * H);
-    return hipGetLastError();
-}
-
-hipError_t launch_fa_int8_fused_main(const Int8Workspace& w, int* cnt, const float* Qf, const float* Kf,
-                                     const float* Vf, float* O, int B, int N, int H, int d_model, int hpx, int delta,
-                                     int produce, hipStream_t stream) {
-    const FuseArgs fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, cnt, hpx, delta, produce};
-    return fa_int8_pipe_launch<64, 4, kD64Flags | FL_FUSE>(w, Qf, O, B, N, H, d_model, stream, QkDump{}, fz);
 }
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,

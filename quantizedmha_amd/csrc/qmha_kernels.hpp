@@ -42,29 +42,6 @@ struct QkDump {
     int8_t* Qi;
     float* sQ;
 };
-// the fused int8 path (qmha_fa_int8_pipe_kernel FL_FUSE): main-kernel workgroups quantise the
-// K/V of a later head on their XCD while the main kernels of earlier heads compute
-struct FuseArgs {
-    const float* Kf;
-    const float* Vf;
-    int8_t* Ki;
-    _Float16* Vh;
-    float* sK;
-    float* sV;
-    int* cnt;   // per-head count of producer workgroups done
-    int hpx;    // heads per XCD run of workgroups
-    int delta;  // a workgroup of head h produces (its share of) head h + delta
-    int produce;  // 0: producers skipped, every later head takes the fallback (test hook)
-};
-// fused int8 path: whether the shape qualifies (d = 64, whole heads per XCD run of workgroups),
-// the pre-launch (K/V of the first `delta` heads of every run; zeroes cnt[0, B*H)) and the
-// fused main kernel
-bool fa_int8_fused_plan(int B, int N, int H, int D, int* hpx, int* delta);
-hipError_t launch_fa_int8_fused_pre(const Int8Workspace& w, int* cnt, const float* Kf, const float* Vf, int B, int N,
-                                    int H, int d_model, int hpx, int delta, hipStream_t stream);
-hipError_t launch_fa_int8_fused_main(const Int8Workspace& w, int* cnt, const float* Qf, const float* Kf,
-                                     const float* Vf, float* O, int B, int N, int H, int d_model, int hpx, int delta,
-                                     int produce, hipStream_t stream);
 hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, QkDump dbg, hipStream_t stream);
 

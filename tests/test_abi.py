@@ -139,8 +139,7 @@ def test_slot_permutations_are_bijective():
 
 def test_production_library_has_one_kernel_per_variant_and_d(built):
     """No tuning/ablation alternates in the shipped libqmha.so (round-1 ADVICE): every kernel
-    template is instantiated at most once per head size (plus the FL_DUMP / FL_FUSE twins of the
-    production int8 schedule), and no QMHA_*_CFG / overlap
+    template is instantiated at most once per head size, and no QMHA_*_CFG / overlap
     environment switch exists (those live in QMHA_ABLATION builds only)."""
     path = os.path.join(LIB_DIR, "libqmha.so")
     syms = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
@@ -151,10 +150,8 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
         if name.startswith("qmha_gemm"):
             continue
         m = re.match(r"Li(\d+)ELi(\d+)E", rest) if name == "qmha_fa_int8_pipe_kernel" else None
-        # FL_DUMP (256: the test-hook twin) and FL_FUSE (1024: the fused-quantisation twin, same
-        # schedule plus the in-kernel K/V producer) of the production instance
-        if m and int(m.group(2)) & (256 | 1024):
-            dumps.append((d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~(256 | 1024)}E", 1)))
+        if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
+            dumps.append((d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
             continue
         per.setdefault((name, d), set()).add(rest)
     assert dumps
