@@ -154,3 +154,54 @@ def test_shard_gpu_world1():
     out = solve_sharded(Q, K, V, 256, 4, "fa_tc_int8_b")
     ref = torch_ext.flash_solve(Q, K, V, 256, 4, "fa_tc_int8_b")
     assert torch.equal(out, ref)
+
+
+def _gpu_worker(rank, world, port, B, result_path):
+    """One rank of a world-2 job on the box's single GPU: the HIP kernel computes this rank's
+    shard on cuda:0; the all-gather runs over gloo on host copies (RCCL needs one GPU per rank)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizedmha_amd import torch_ext
+        dev = torch.device("cuda:0")
+
+        def solve_fn(Q, K, V, d_model, h, kernel):
+            return torch_ext.flash_solve(Q.to(dev), K.to(dev), V.to(dev), d_model, h, kernel).cpu()
+
+        Q, K, V = _inputs(B, 256, 256)
+        start, stop = batch_shard(B, rank, world)
+        sh = [t[start:stop].clone() for t in (Q, K, V)]
+        outs = {f"int8_chunks{c}": solve_sharded(*sh, 256, 4, "fa_tc_int8_b", batch=B, chunks=c, solve_fn=solve_fn)
+                for c in (1, 2)}
+        outs["fp16"] = solve_sharded(*sh, 256, 4, "fa_tc_v1a", batch=B, solve_fn=solve_fn)
+        if rank == 0:
+            torch.save(outs, result_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [4, 5])
+def test_shard_hip_world2(tmp_path, B):
+    """The batch-shard path with world > 1 driving the HIP kernels: two ranks (gloo), each
+    computing its own shard with flash_solve on the GPU, chunked all-gather; the gathered
+    output equals one unsharded launch bit for bit (even and uneven shards)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    path = str(tmp_path / "out.pt")
+    env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    try:
+        mp.start_processes(_gpu_worker, args=(2, _free_port(), B, path), nprocs=2, join=True, start_method="spawn")
+    finally:
+        if env_keep is None:
+            os.environ.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
+    res = torch.load(path, weights_only=True)
+    from quantizedmha_amd import torch_ext
+    dev = torch.device("cuda:0")
+    Q, K, V = (t.to(dev) for t in _inputs(B, 256, 256))
+    ref8 = torch_ext.flash_solve(Q, K, V, 256, 4, "fa_tc_int8_b").cpu()
+    ref16 = torch_ext.flash_solve(Q, K, V, 256, 4, "fa_tc_v1a").cpu()
+    for key, out in res.items():
+        assert out.shape == (B, 256, 256), key
+        assert torch.equal(out, ref16 if key == "fp16" else ref8), key
