@@ -428,6 +428,149 @@ __global__ __launch_bounds__(NT) void qmha_fa_f32_v3_kernel(const float* __restr
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// v4: the same contract on the fp32 matrix cores.  v_mfma_f32_32x32x2_f32 (exact fp32
+// products, fp32 accumulation; 64 FLOP/clk/SIMD, the fp32 vector rate) for both products, so
+// the FMAs leave the VALU and the LDS operand traffic per FLOP drops 32x.  One workgroup = 4
+// waves = 128 query rows of one head, one 32-row group per wave; swapped products as in the
+// int8/fp16 kernels: S^T = K Q^T (lane (q, h) holds 16 keys of query q), O^T = V^T P^T with P^T
+// straight from the S^T accumulator (step r of P@V takes accumulator register r; its two keys
+// 8(r/4) + 4h + r%4 select the V^T operand).  The d order of the Q.K dot is d = s + h D/2 (lane
+// half h supplies the second k-entry of each 32x32x2 step), the key order of P.V is the
+// accumulator's: both differ from fa.cu's sequential fmaf chains only by fp32 rounding order.
+// Softmax arithmetic as v3 (scores * 1/sqrt(d), m0 = 0, alpha, l = fma(alpha, l, rowsum),
+// O = O*alpha + PV, guard 1e-10).
+// ---------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256, D == 128 ? 2 : 3) void qmha_fa_f32_mfma_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, float* __restrict__ O,
+    int N, int H, int d_model, float inv_sqrt_d) {
+    constexpr int HD = D / 2, MB = D / 32;
+    constexpr int KST = D + 4;  // K rows (floats): b128 reads of 32 rows spread over the banks
+    constexpr int VST = 36;     // V^T rows [D][32 keys + 4]
+    constexpr int LD = 32 * D / 4 / 256;  // float4 of K (and of V) per thread per tile
+    static_assert(LD >= 1, "d >= 32");
+    __shared__ __attribute__((aligned(16))) float kl[32 * KST];
+    __shared__ __attribute__((aligned(16))) float vt[D * VST];
+
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + 3) / 4;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int qg = qb * 4 + wave;
+    const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
+    const size_t head_off = (size_t)b * N * d_model + (size_t)k * D;
+
+    float qop[HD];  // Q[q][h D/2 + s], s < D/2: the B operand of Q.K step s
+    {
+        const float* qrow = Q + head_off + (size_t)(qg * QMHA_GROUP + col) * d_model + half * HD;
+#pragma unroll
+        for (int j = 0; j < HD / 4; ++j) {
+            v4f x = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (active) x = *reinterpret_cast<const v4f*>(qrow + 4 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qop[4 * j + e] = x[e];
+        }
+    }
+    v16f o[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) o[m] = v16f{};
+    float m_prev = 0.0f, l = 0.0f;  // m0 = 0 (fa.cu:279)
+
+    v4f kreg[LD], vreg[LD];
+    auto gload = [&](int t) {
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+            const int i = tid + 256 * j, row = i / (D / 4), c4 = i % (D / 4);
+            const size_t g = head_off + (size_t)(t * 32 + row) * d_model + 4 * c4;
+            kreg[j] = *reinterpret_cast<const v4f*>(K + g);
+            vreg[j] = *reinterpret_cast<const v4f*>(V + g);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int j = 0; j < LD; ++j) {
+            const int i = tid + 256 * j, row = i / (D / 4), c4 = i % (D / 4);
+            *reinterpret_cast<v4f*>(&kl[row * KST + 4 * c4]) = kreg[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vt[(4 * c4 + e) * VST + row] = vreg[j][e];
+        }
+    };
+
+    gload(0);
+    for (int t = 0; t < G; ++t) {
+        __syncthreads();  // the previous tile's kl / vt reads are done
+        lstore();
+        __syncthreads();
+        if (t + 1 < G) gload(t + 1);  // in flight during this tile's MFMAs
+        // ---- S^T = K Q^T (fa.cu:24-102), then * 1/sqrt(d) (:141)
+        v16f s = v16f{};
+#pragma unroll
+        for (int j = 0; j < HD / 4; ++j) {
+            const v4f kv = *reinterpret_cast<const v4f*>(&kl[col * KST + half * HD + 4 * j]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[e], qop[4 * j + e], s, 0, 0, 0);
+        }
+        // ---- online softmax (fa.cu:106-209): 16 keys per lane, the two lane halves joined
+        float mx = m_prev;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            s[r] *= inv_sqrt_d;
+            mx = fmaxf(mx, s[r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float p[16], rs = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            p[r] = exp_e(s[r] - mx);  // fa.cu:167
+            rs += p[r];
+        }
+        rs += __shfl_xor(rs, 32);
+        const float alpha = exp_e(m_prev - mx);  // fa.cu:187
+        l = fmaf(alpha, l, rs);                   // fa.cu:190
+        m_prev = mx;
+        // ---- O = alpha*O + P V (fa.cu:93-94,199)
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            v16f a = v16f{};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const v4f vv = *reinterpret_cast<const v4f*>(&vt[(32 * m + col) * VST + 8 * j + 4 * half]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[e], p[4 * j + e], a, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[m][r] = __fadd_rn(__fmul_rn(o[m][r], alpha), a[r]);
+        }
+    }
+    if (!active) return;
+    // lane (q, h) holds O^T rows d = 32 m + 8 g + 4 h + e (e < 4) of query q
+    const bool ok = l > 1e-10f;  // fa.cu:371
+    float* orow = O + head_off + (size_t)(qg * QMHA_GROUP + col) * d_model + 4 * half;
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            v4f w;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = ok ? o[m][4 * g4 + e] / l : 0.0f;
+            *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
+        }
+}
+
+template <int D>
+static hipError_t fa_f32_mfma(const float* Q, const float* K, const float* V, float* O, int B, int N, int H,
+                              int d_model, hipStream_t stream) {
+    const int G = N / QMHA_GROUP;
+    const float inv_sqrt_d = 1.0f / sqrtf((float)D);  // fa.cu:410
+    hipLaunchKernelGGL((qmha_fa_f32_mfma_kernel<D>), dim3(B * H * ((G + 3) / 4)), dim3(256), 0, stream, Q, K, V, O, N,
+                       H, d_model, inv_sqrt_d);
+    return hipGetLastError();
+}
+
 template <int D>
 static hipError_t fa_f32_v2(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream) {
@@ -469,15 +612,16 @@ hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* 
             case 37: return fa_f32_v3<64, 2, 128>(Q, K, V, O, B, N, H, d_model, stream);
             case 1: return fa_f32_d<64>(Q, K, V, O, B, N, H, d_model, stream);
             case 2: return fa_f32_v2<64>(Q, K, V, O, B, N, H, d_model, stream);
+            case 3: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
             default: break;
         }
     }
 #endif
-    // d = 64: v3 (4 rows x 4 keys per thread, 256 threads = 128 rows per workgroup); else v2
+    // every d: v4 on the fp32 matrix cores (128 query rows per workgroup)
     switch (D) {
-        case 32: return fa_f32_v2<32>(Q, K, V, O, B, N, H, d_model, stream);
-        case 64: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
-        case 128: return fa_f32_v2<128>(Q, K, V, O, B, N, H, d_model, stream);
+        case 32: return fa_f32_mfma<32>(Q, K, V, O, B, N, H, d_model, stream);
+        case 64: return fa_f32_mfma<64>(Q, K, V, O, B, N, H, d_model, stream);
+        case 128: return fa_f32_mfma<128>(Q, K, V, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }
