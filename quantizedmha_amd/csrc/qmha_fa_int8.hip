@@ -213,7 +213,8 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //               the bit-exact check of the production Q@K^T path; never the production launch)
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
        FL_DUMP = 256, FL_PIN = 512,
-       FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096 };
+       FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -501,7 +502,11 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
-    constexpr int SG = 2, RING = 3;
+    // FL_RING4 (d = 64): a 4-slot ring filled three stages ahead; the stage barrier waits with a
+    // counted vmcnt (the newest stage's pieces stay in flight across it) instead of vmcnt(0)
+    constexpr bool RING4 = FL & FL_RING4;
+    static_assert(!RING4 || D == 64, "FL_RING4: the counted wait assumes 3 pieces per wave and stage (d = 64)");
+    constexpr int SG = 2, RING = RING4 ? 4 : 3, PF = RING - 1;  // PF: stages in flight ahead
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
     constexpr int SBYTES = KBYTES + VBYTES;
@@ -561,22 +566,26 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
     }
     // stage st into ring slot `slot` (= st % RING; a compile-time constant in the unrolled loop)
-    auto issue_at = [&](int st, int slot) {
+    // piece `pc` (< KJ + VJ: this wave's K pieces, then its V pieces) of stage st into ring slot
+    // `slot`; pieces < 0 = all of them
+    auto issue_piece = [&](int st, int slot, int pc) {
+        if constexpr (FL & FL_ABL_NODMA) return;  // timing perturbation: stages never refilled
         const int ngr = min(SG, G - st * SG);
         int8_t* L = lds[slot];
 #pragma unroll
         for (int jj = 0; jj < KJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
+            if ((pc < 0 || pc == jj) && inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
                 buffer_load_lds16(kbase, N * D, (lptr_t)(L + inst * 1024), koff[jj], st * KBYTES);
         }
 #pragma unroll
         for (int jj = 0; jj < VJ; ++jj) {
             const int inst = wave + jj * WAVES;
-            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
+            if ((pc < 0 || pc == KJ + jj) && inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
                 buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
+    auto issue_at = [&](int st, int slot) { issue_piece(st, slot, -1); };
     auto issue = [&](int st) { issue_at(st, st % RING); };
     // operand reads of the tile in ring slot `slot`, position `par` (0/1) of its stage
     auto kop_at = [&](int slot, int par, int ks) {
@@ -627,9 +636,10 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
     float anchor = 0.0f;
     v16i s_cur, s_nxt;           // S^T of tiles t and t+1
-    // FL_ABL_NOMFMA / FL_ABL_NOEXP (timing perturbations, QMHA_ABLATION builds only; results are
-    // wrong): every MFMA / every exp of the softmax replaced by an empty asm that keeps its
-    // operands and result live, so the rest of the loop compiles to the same VALU work
+    // FL_ABL_NOMFMA / FL_ABL_NOEXP / FL_ABL_NODMA (timing perturbations, A/B builds only; results
+    // are wrong): every MFMA / every exp of the softmax replaced by an empty asm that keeps its
+    // operands and result live, so the rest of the loop compiles to the same VALU work / no
+    // LDS-DMA issued (barriers and operand reads unchanged)
     constexpr bool NOMFMA = FL & FL_ABL_NOMFMA, NOEXP = FL & FL_ABL_NOEXP;
     auto qk = [&](const v4i& kk, int ks) {
         if constexpr (NOMFMA) {
@@ -693,6 +703,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
 
     issue(0);
     if (nst > 1) issue(1);
+    if (RING4 && nst > 2) issue(2);
     qmha_dma_barrier();
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qk(kop_of(0, ks), ks);
@@ -714,10 +725,31 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
         auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
         auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
+        // FL_DMA_SPLIT: the stage's LDS-DMA pieces issue one after each of the first MFMAs of the
+        // iteration (in the MFMA's shadow) instead of together right after the barrier
+        constexpr bool SPLIT = FL & FL_DMA_SPLIT;
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        const bool dma_now = odd && dma_st < nst;  // uniform
+        auto dma_piece = [&](int pc) {
+            if constexpr (SPLIT)
+                if (dma_now && pc < KJ + VJ) issue_piece(dma_st, dma_slot, pc);
+        };
         if (odd) {  // uniform
-            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
-            if ((t >> 1) + 2 < nst)
-                issue_at((t >> 1) + 2, ph >= 0 ? ((((1 + ph) >> 1) + 2) % RING) : (((t >> 1) + 2) % RING));
+            if constexpr (RING4) {
+                // stage (t+1)/2 must have landed; stage (t+1)/2 + 1 (this wave's 3 pieces, issued
+                // last) may stay in flight unless it is the (possibly partial) last stage
+                const int s1 = (t + 1) / 2 + 1;
+                if (s1 < nst - 1 || (s1 == nst - 1 && G % SG == 0))
+                    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // raw barrier: __syncthreads' workgroup fence would add a vmcnt(0) of its own
+                __builtin_amdgcn_s_barrier();
+            } else {
+                qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            }
+            if (!SPLIT && dma_now) issue_at(dma_st, dma_slot);
         }
         if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (32x32 accumulator map)
             if (active) {
@@ -784,6 +816,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
             anchor = m_new;
         }
         mfmas(0);
+        dma_piece(0);
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
@@ -801,6 +834,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         if constexpr (PIN) pin_regs(x, 0, 8);
         QMHA_FENCE();
         mfmas(1);
+        dma_piece(1);
         QMHA_FENCE();
         // ---- C: scores of rows 8..15
 #pragma unroll
@@ -815,6 +849,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         if constexpr (PIN) pin_regs(x, 8, 16);
         QMHA_FENCE();
         mfmas(2);
+        dma_piece(2);
         QMHA_FENCE();
         // ---- D: p = exp2, rows 0..7
         float p[16];
@@ -891,13 +926,18 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     using DYN = std::integral_constant<int, -1>;
     iter(0, F0{}, T1{}, DYN{});
     int t = 1;
-    for (; t + 6 <= G - 1; t += 6) {
+    constexpr int PER = 2 * RING;  // ring period in tiles
+    for (; t + PER <= G - 1; t += PER) {
         iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
         iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
         iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
         iter(t + 3, T1{}, T1{}, std::integral_constant<int, 3>{});
         iter(t + 4, T1{}, T1{}, std::integral_constant<int, 4>{});
         iter(t + 5, T1{}, T1{}, std::integral_constant<int, 5>{});
+        if constexpr (RING4) {
+            iter(t + 6, T1{}, T1{}, std::integral_constant<int, 6>{});
+            iter(t + 7, T1{}, T1{}, std::integral_constant<int, 7>{});
+        }
     }
     for (; t < G - 1; ++t) iter(t, T1{}, T1{}, DYN{});
     iter(G - 1, T1{}, F0{}, DYN{});

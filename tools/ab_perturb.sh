@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export PYTHONUNBUFFERED=1
 OUT=gpurun_out/${1:-perturb}; mkdir -p $OUT
-for lib in default nomfma noexp default nomfma noexp; do
+for lib in ${LIBS:-default nomfma noexp default nomfma noexp}; do
   if [ "$lib" = default ]; then LP=""; else LP=$PWD/quantizedmha_amd/alt_lib/$lib/libqmha.so; fi
   QMHA_LIB_PATH=$LP timeout -k 10 180 python bench.py --no-siblings --no-cpu-baseline --no-refconfig --no-solve-calls > $OUT/bench_$lib.json 2> $OUT/bench_$lib.err
   rc=$?; [ $rc -ne 0 ] && { echo "bench $lib rc=$rc"; tail -3 $OUT/bench_$lib.err; exit $rc; }
