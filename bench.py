@@ -32,8 +32,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x bf16 2.5 PF; MI355X_MICROARCH.md)
 F16_PEAK_TFLOPS = 2500.0
 F32_VALU_PEAK_TFLOPS = 157.3
+F32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 runs at the fp32 vector rate (MI355X_MICROARCH.md)
 PEAKS = {"fa_tc_int8_b": INT8_PEAK_TOPS, "fa_tc_v1a": F16_PEAK_TFLOPS, "fa": F32_VALU_PEAK_TFLOPS,
-         "unfused": F32_VALU_PEAK_TFLOPS}
+         "fa_mfma": F32_MFMA_PEAK_TFLOPS, "unfused": F32_VALU_PEAK_TFLOPS}
+PEAK_KIND = {"fa_tc_int8_b": "int8 MFMA", "fa_tc_v1a": "f16 MFMA", "fa": "fp32 VALU (no matrix cores)",
+             "fa_mfma": "fp32 MFMA", "unfused": "fp32 MFMA GEMMs"}
 
 
 def flops(B, H, N, d):
@@ -347,12 +350,14 @@ def main():
     side = {}
     if not a.no_siblings and not dry:
         sib = {}
-        # fa_tc_v1a at C3 (= the C4 shape), fa at C2, and the reference's unfused 3-kernel baseline
+        # fa_tc_v1a at C3 (= the C4 shape), fa (the scalar no-matrix-core kernel BASELINE C2 names)
+        # and its fp32-MFMA sibling fa_mfma at C2, and the reference's unfused 3-kernel baseline
         # (README.md:11, the fused-vs-unfused comparison) at the C4 shape
-        for v in ("fa_tc_v1a", "fa", "unfused"):
-            Bs = B if v != "fa" else 8
-            Hs = H if v != "fa" else 8
-            Ns = N if v != "fa" else 1024
+        for v in ("fa_tc_v1a", "fa", "fa_mfma", "unfused"):
+            c2 = v in ("fa", "fa_mfma")
+            Bs = B if not c2 else 8
+            Hs = H if not c2 else 8
+            Ns = N if not c2 else 1024
             # the first side measurement also absorbs the clock ramp of a fresh process
             steps_v, warm_v = (max(3, a.steps // 2), 10 if v == "fa_tc_v1a" else 2) if v != "unfused" else (3, 1)
             rv = run_variant(v, Bs, Hs, Ns, d, steps_v, warm_v, dev, rank, world)
@@ -360,7 +365,8 @@ def main():
                       "tflops": round(flops(Bs, Hs, Ns, d) * world / (rv["ms_per_step"] * 1e-3) / 1e12, 3),
                       "main_kernel_ms": round(rv["main_kernel_ms"], 4),
                       "roofline_frac": round(flops(Bs, Hs, Ns, d) / (rv["main_kernel_ms"] * 1e-3) / 1e12 /
-                                             PEAKS[v], 4)}
+                                             PEAKS[v], 4),
+                      "peak": f"{PEAKS[v]} TFLOP/s {PEAK_KIND[v]}"}
             del rv
         side["siblings"] = sib
     if not a.no_refconfig and not dry and world == 1:

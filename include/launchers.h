@@ -10,6 +10,7 @@
  *   libqmha_fa_tc_int8_b.so    `solve` bound to the INT8 path      (make KERNEL=fa_tc_int8_b)
  *   libqmha_fa_tc_v1a.so       `solve` bound to the FP16 MFMA path (make KERNEL=fa_tc_v1a)
  *   libqmha_fa.so              `solve` bound to the scalar path    (make KERNEL=fa)
+ *   libqmha_fa_mfma.so         `solve` bound to fa's contract on the fp32 matrix cores
  *   libqmha_unfused.so         `solve` bound to the 3-kernel path  (make KERNEL=unfused)
  * mirroring the reference's one-kernel-per-binary build (Makefile:39-53,
  * extensions/torch/setup.py:21-43).
@@ -29,7 +30,9 @@ typedef enum {
     QMHA_FA = 0,           /* mha_kernels/fa.cu         : fp32 scalar, no matrix cores   */
     QMHA_FA_TC_V1A = 1,    /* mha_kernels/fa_tc_v1a.cu  : fp16 MFMA, fp32 accumulation   */
     QMHA_FA_TC_INT8_B = 2, /* mha_kernels/fa_tc_int8_b.cu: int8 MFMA, per-32-row scales  */
-    QMHA_UNFUSED = 3       /* mha_kernels/unfused.cu    : QK^T, softmax, PV (3 kernels)   */
+    QMHA_UNFUSED = 3,      /* mha_kernels/unfused.cu    : QK^T, softmax, PV (3 kernels)   */
+    QMHA_FA_MFMA = 4       /* fa.cu's fp32 contract on v_mfma_f32_32x32x2_f32 (no reference
+                              counterpart: the matrix-core sibling of the scalar `fa`)    */
 } qmha_variant_t;
 
 /* Status codes of the extended entry points. */
@@ -108,7 +111,7 @@ int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int 
 int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                             int h, int32_t *S, int8_t *Qi, float *sQ);
 
-/* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused") -> id, or -1. */
+/* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma") -> id, or -1. */
 int qmha_variant_from_name(const char *name);
 const char *qmha_variant_name(int variant);
 const char *qmha_status_string(int status);
@@ -120,7 +123,7 @@ const char *qmha_last_error(void);
  * Kernel timing for roofline reporting (bench.py): when enabled, qmha_solve_* record a
  * hipEvent pair around every launch of the dominant ("main") kernel and of the pre-pass.
  * The int8 and fp16 paths split a call into batch chunks whose pre-pass runs on a library
- * stream, overlapped with the previous chunk's main kernel (QMHA_OVERLAP_CHUNKS, default 1 = off).
+ * stream, overlapped with the previous chunk's main kernel (qmha_set_overlap_chunks, default 1 = off).
  * qmha_profile_collect synchronises those events and returns the summed main-kernel and
  * pre-pass milliseconds and the number of calls since the last collect, then clears the record.
  */

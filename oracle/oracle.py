@@ -120,7 +120,8 @@ def fa_fp32(Q, K, V, d_model, h, nthreads=0):
     return _run4(lib().oracle_fa_fp32, Q, K, V, d_model, h, nthreads)
 
 
-ORACLE_BY_VARIANT = {"fa_tc_int8_b": fa_int8, "fa_tc_v1a": fa_fp16, "fa": fa_fp32, "unfused": cpu_attention}
+ORACLE_BY_VARIANT = {"fa_tc_int8_b": fa_int8, "fa_tc_v1a": fa_fp16, "fa": fa_fp32, "unfused": cpu_attention,
+                     "fa_mfma": fa_fp32}
 
 
 def cpu_reference_rope(Q, K, V, d_model, h):

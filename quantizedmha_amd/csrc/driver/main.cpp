@@ -44,7 +44,7 @@ static void usage(const char* argv0) {
         "Usage: %s [--kernel=KERNEL] [--warmup=N] [--runs=M] [--check=0|1] [--no-check] [--random]\n"
         "          [--B=1] [--N=8192] [--d_model=1024] [--h=32] [--check-random] [--threads=T]\n"
         "          [--cache-dir=.cache] [--json]\n"
-        "  KERNEL options: fa, fa_tc_v1a, fa_tc_int8_b, unfused\n",
+        "  KERNEL options: fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma\n",
         argv0);
 }
 

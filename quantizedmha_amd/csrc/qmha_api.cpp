@@ -58,7 +58,7 @@ int check_shape(const void* Q, const void* K, const void* V, const void* O, int 
         g_last_error = "head size d = d_model/h must be 32, 64 or 128";
         return QMHA_ERR_NOSYS;
     }
-    if (variant < QMHA_FA || variant > QMHA_UNFUSED) {
+    if (variant < QMHA_FA || variant > QMHA_FA_MFMA) {
         g_last_error = "unknown variant";
         return QMHA_ERR_INVALID;
     }
@@ -193,7 +193,7 @@ size_t workspace_bytes(int B, int N, int H, int D, int variant) {
 
 qmha::Int8Workspace int8_slice(const qmha::Int8Workspace& w, size_t b0, int N, int H, int D) {
     const size_t e = b0 * H * N * D, g = b0 * H * (N / 32);  // 32-row quantisation groups
-    return qmha::Int8Workspace{w.Qi + e, w.Ki + e, w.Vh + e, w.sQ + g, w.sK + g, w.sV + g};
+    return qmha::Int8Workspace{nullptr, w.Ki + e, w.Vh + e, nullptr, w.sK + g, w.sV + g};
 }
 qmha::F16Workspace f16_slice(const qmha::F16Workspace& w, size_t b0, int N, int H, int D) {
     const size_t e = b0 * H * N * D;
@@ -277,9 +277,10 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             }
             QMHA_MARK(rec.main, stream, false);
         }
-    } else if (variant == QMHA_FA) {
+    } else if (variant == QMHA_FA || variant == QMHA_FA_MFMA) {
         QMHA_MARK(rec.main, stream, true);
-        QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, stream), "fa_f32 launch");
+        QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, variant == QMHA_FA_MFMA, stream),
+                     "fa_f32 launch");
         QMHA_MARK(rec.main, stream, false);
     } else if (variant == QMHA_UNFUSED) {
         QMHA_MARK(rec.main, stream, true);
@@ -389,11 +390,11 @@ int qmha_debug_qk_int32(const float* Q, const float* K, int N, int d_model, int 
         g_last_error = "head out of range";
         return QMHA_ERR_INVALID;
     }
-    const size_t need = qmha::int8_workspace_bytes(1, N, h, D);
+    const size_t need = qmha::int8_workspace_bytes(1, N, h, D, /*with_q=*/true);
     void* ws = nullptr;
     st = get_workspace(need, nullptr, &ws);
     if (st != QMHA_OK) return st;
-    qmha::Int8Workspace w = qmha::int8_carve(ws, 1, N, h, D);
+    qmha::Int8Workspace w = qmha::int8_carve(ws, 1, N, h, D, /*with_q=*/true);
     QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, Q, w, w.Vh, 1, 1, N, h, D, d_model, nullptr), "quant_int8 launch");
     QMHA_HIP_TRY(qmha::launch_debug_qk_int32(w, N, D, head, S, nullptr), "debug_qk launch");
     QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
@@ -428,6 +429,7 @@ int qmha_variant_from_name(const char* name) {
     if (!std::strcmp(name, "fa_tc_v1a")) return QMHA_FA_TC_V1A;
     if (!std::strcmp(name, "fa_tc_int8_b")) return QMHA_FA_TC_INT8_B;
     if (!std::strcmp(name, "unfused")) return QMHA_UNFUSED;
+    if (!std::strcmp(name, "fa_mfma")) return QMHA_FA_MFMA;
     return -1;
 }
 
@@ -437,6 +439,7 @@ const char* qmha_variant_name(int v) {
         case QMHA_FA_TC_V1A: return "fa_tc_v1a";
         case QMHA_FA_TC_INT8_B: return "fa_tc_int8_b";
         case QMHA_UNFUSED: return "unfused";
+        case QMHA_FA_MFMA: return "fa_mfma";
         default: return "unknown";
     }
 }

@@ -1,17 +1,14 @@
-// qmha_fa_f32.hip -- scalar fp32 FlashAttention forward (no matrix cores), gfx950.
-//
-// Drop-in for the reference's fa (mha_kernels/fa.cu:211-425): fp32 operands, LDS tiling
-// only, Bc = 32 online softmax with m0 = 0 (:279), epilogue guard 1e-10 (:371).
-// Numerics follow fa.cu exactly where the order is defined by the reference:
+// qmha_fa_f32.hip -- fp32 FlashAttention forward for gfx950: the reference's `fa`
+// (mha_kernels/fa.cu:211-425) as a scalar kernel (variant fa: fp32 operands, VALU fmaf, LDS
+// tiling only -- BASELINE config 2 "no tensor cores") and the same contract on the fp32 matrix
+// cores (variant fa_mfma).  Both: Bc = 32 online softmax with m0 = 0 (:279), epilogue guard
+// 1e-10 (:371).  The scalar kernel follows fa.cu's summation order exactly:
 //   S[r][j]  = fmaf chain over k = 0..d-1 from 0 (matmul_warp_tiled, :63-86 under nvcc's
 //              default FMA contraction), then * (1/sqrt(d))          -> bit-identical S
 //   O[r][:] *= alpha;  O[r][c] += (fmaf chain over the tile's 32 kv of P*V)  (:93-94)
 // exp is exp2(x * log2 e) on v_exp_f32 (2 VALU ops; OCML's expf is ~13 per element with its
 // range checks, and its SGPR constants run at the slow issue rate): p differs from the
 // reference's expf by ~1e-6 relative, so O agrees with the oracle to ~1e-6, not bitwise.
-//
-// One workgroup = 32 query rows of one (batch, head), 256 threads = 4 wave64; thread
-// (r = tid/8, c = tid%8) owns S[r][c + 8j] (j < 4) and O[r][c + 8j] (j < D/8).
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
@@ -21,256 +18,17 @@ namespace qmha {
 // |x| < 30 a softmax sees before p underflows), v_exp_f32 itself ~1 ulp
 __device__ __forceinline__ float exp_e(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
-template <int D>
-__global__ __launch_bounds__(256) void qmha_fa_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K,
-                                                          const float* __restrict__ V, float* __restrict__ O, int N,
-                                                          int H, int d_model, float inv_sqrt_d) {
-    constexpr int DP = D + 1;  // padded row: column reads of K are conflict-free
-    constexpr int OPT = D / 8;
-    __shared__ float qs[32 * D];
-    __shared__ float ks[32 * DP];
-    __shared__ float vs[32 * D];
-    __shared__ float ps[32 * 33];
-
-    const int G = N / QMHA_GROUP;
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = wg / G, qg = wg % G;
-    const int b = bh / H, k = bh % H;
-    const int tid = threadIdx.x, r = tid >> 3, c = tid & 7;
-    const size_t head_off = (size_t)b * N * d_model + (size_t)k * D;
-
-    for (int i = tid; i < 32 * D / 4; i += 256) {
-        const int row = i / (D / 4), c4 = i % (D / 4);
-        *reinterpret_cast<v4f*>(&qs[row * D + 4 * c4]) =
-            *reinterpret_cast<const v4f*>(Q + head_off + (size_t)(qg * 32 + row) * d_model + 4 * c4);
-    }
-    float o[OPT];
-#pragma unroll
-    for (int j = 0; j < OPT; ++j) o[j] = 0.0f;
-    float m_prev = 0.0f, l = 0.0f;
-
-    for (int t = 0; t < G; ++t) {
-        __syncthreads();  // previous tile's ks/vs/ps reads are done
-        for (int i = tid; i < 32 * D / 4; i += 256) {
-            const int row = i / (D / 4), c4 = i % (D / 4);
-            const size_t g = head_off + (size_t)(t * 32 + row) * d_model + 4 * c4;
-            const v4f kv = *reinterpret_cast<const v4f*>(K + g);
-            const v4f vv = *reinterpret_cast<const v4f*>(V + g);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) ks[row * DP + 4 * c4 + e] = kv[e];
-            *reinterpret_cast<v4f*>(&vs[row * D + 4 * c4]) = vv;
-        }
-        __syncthreads();
-        float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int kk = 0; kk < D; ++kk) {
-            const float qv = qs[r * D + kk];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s[j] = fmaf(qv, ks[(c + 8 * j) * DP + kk], s[j]);
-        }
-        float mx = m_prev;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            s[j] *= inv_sqrt_d;  // fa.cu:141
-            mx = fmaxf(mx, s[j]);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 1));
-        mx = fmaxf(mx, __shfl_xor(mx, 2));
-        mx = fmaxf(mx, __shfl_xor(mx, 4));
-        float rs = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float p = exp_e(s[j] - mx);  // fa.cu:167
-            ps[r * 33 + c + 8 * j] = p;
-            rs += p;
-        }
-        rs += __shfl_xor(rs, 1);
-        rs += __shfl_xor(rs, 2);
-        rs += __shfl_xor(rs, 4);
-        const float alpha = exp_e(m_prev - mx);  // fa.cu:187
-        l = fmaf(alpha, l, rs);                 // fa.cu:190
-        m_prev = mx;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < OPT; ++j) {
-            const int d = c + 8 * j;
-            float acc = 0.0f;
-#pragma unroll 8
-            for (int kv = 0; kv < 32; ++kv) acc = fmaf(ps[r * 33 + kv], vs[kv * D + d], acc);
-            o[j] = __fadd_rn(__fmul_rn(o[j], alpha), acc);  // fa.cu:199 then :94 (C += acc), no contraction
-        }
-    }
-    float* orow = O + head_off + (size_t)(qg * 32 + r) * d_model;
-    const bool ok = l > 1e-10f;
-#pragma unroll
-    for (int j = 0; j < OPT; ++j) orow[c + 8 * j] = ok ? o[j] / l : 0.0f;
-}
-
 // ---------------------------------------------------------------------------------------
-// v2: register-tiled.  One workgroup = 64 query rows of one (batch, head), 256 threads; thread
-// (rp = tid / 8, c = tid % 8) owns rows {rp, rp + 32}.  S phase: columns 4c..4c+3 of the 32-key
-// tile, K kept transposed in LDS so the four keys come in one ds_read_b128; Q read four k at a
-// time.  P@V phase: output columns {32h + 4c .. 32h + 4c + 3}.  Per FMA the LDS traffic drops
-// from 1.25 scalar reads (v1) to ~0.19 b128 reads; every S and P@V sum keeps the reference's
-// sequential fmaf order (bit-identical S, same O arithmetic as v1).  K/V of tile t+1 are
-// prefetched into registers while tile t computes.
-// ---------------------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256) void qmha_fa_f32_v2_kernel(const float* __restrict__ Q, const float* __restrict__ K,
-                                                             const float* __restrict__ V, float* __restrict__ O, int N,
-                                                             int H, int d_model, float inv_sqrt_d) {
-    constexpr int QS = D + 4;   // q row stride (floats): b128 row reads hit distinct banks
-    constexpr int KTS = 36;     // transposed K: [D][32 keys + 4]
-    constexpr int VS = D + 4;   // V rows
-    constexpr int PS = 36;      // P rows [64][32 + 4]
-    constexpr int CH = D / 32;  // 4-column output chunks per thread
-    constexpr int LD = 32 * D / 4 / 256;  // float4 of K (and of V) per thread per tile
-    static_assert(LD >= 1, "d >= 32");
-    __shared__ __attribute__((aligned(16))) float qs[64 * QS];
-    __shared__ __attribute__((aligned(16))) float kt[D * KTS];
-    __shared__ __attribute__((aligned(16))) float vs[32 * VS];
-    __shared__ __attribute__((aligned(16))) float ps[64 * PS];
-
-    const int G = N / QMHA_GROUP;
-    const int nqb = (G + 1) / 2;  // 64-row query blocks
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = wg / nqb, qb = wg % nqb;
-    const int b = bh / H, k = bh % H;
-    const int tid = threadIdx.x, rp = tid >> 3, c = tid & 7;
-    const size_t head_off = (size_t)b * N * d_model + (size_t)k * D;
-    const int row0 = qb * 64;
-
-    for (int i = tid; i < 64 * D / 4; i += 256) {
-        const int row = i / (D / 4), c4 = i % (D / 4);
-        v4f x = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (row0 + row < N) x = *reinterpret_cast<const v4f*>(Q + head_off + (size_t)(row0 + row) * d_model + 4 * c4);
-        *reinterpret_cast<v4f*>(&qs[row * QS + 4 * c4]) = x;
-    }
-    float o[2][CH][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int h = 0; h < CH; ++h)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[i][h][e] = 0.0f;
-    float m_prev[2] = {0.0f, 0.0f}, l[2] = {0.0f, 0.0f};  // m0 = 0 (fa.cu:279)
-
-    v4f kreg[LD], vreg[LD];
-    auto gload = [&](int t) {
-#pragma unroll
-        for (int j = 0; j < LD; ++j) {
-            const int i = tid + 256 * j, row = i / (D / 4), c4 = i % (D / 4);
-            const size_t g = head_off + (size_t)(t * 32 + row) * d_model + 4 * c4;
-            kreg[j] = *reinterpret_cast<const v4f*>(K + g);
-            vreg[j] = *reinterpret_cast<const v4f*>(V + g);
-        }
-    };
-    auto lstore = [&]() {
-#pragma unroll
-        for (int j = 0; j < LD; ++j) {
-            const int i = tid + 256 * j, row = i / (D / 4), c4 = i % (D / 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) kt[(4 * c4 + e) * KTS + row] = kreg[j][e];
-            *reinterpret_cast<v4f*>(&vs[row * VS + 4 * c4]) = vreg[j];
-        }
-    };
-
-    gload(0);
-    for (int t = 0; t < G; ++t) {
-        __syncthreads();  // the previous tile's kt/vs/ps reads are done
-        lstore();
-        __syncthreads();
-        if (t + 1 < G) gload(t + 1);  // in flight during this tile's compute
-        // ---- S = Q K^T (fa.cu:24-102): sequential fmaf chain over k from 0, then * 1/sqrt(d)
-        float sacc[2][4] = {};
-#pragma unroll 4
-        for (int kk = 0; kk < D; kk += 4) {
-            const v4f q0 = *reinterpret_cast<const v4f*>(&qs[rp * QS + kk]);
-            const v4f q1 = *reinterpret_cast<const v4f*>(&qs[(rp + 32) * QS + kk]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const v4f kv = *reinterpret_cast<const v4f*>(&kt[(kk + e) * KTS + 4 * c]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    sacc[0][j] = fmaf(q0[e], kv[j], sacc[0][j]);
-                    sacc[1][j] = fmaf(q1[e], kv[j], sacc[1][j]);
-                }
-            }
-        }
-        // ---- online softmax per row (fa.cu:106-209); the row's 32 scores live on 8 lanes
-        float alpha[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            float mx = m_prev[i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sacc[i][j] *= inv_sqrt_d;  // fa.cu:141
-                mx = fmaxf(mx, sacc[i][j]);
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 1));
-            mx = fmaxf(mx, __shfl_xor(mx, 2));
-            mx = fmaxf(mx, __shfl_xor(mx, 4));
-            v4f pv;
-            float rs = 0.0f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                pv[j] = exp_e(sacc[i][j] - mx);  // fa.cu:167
-                rs += pv[j];
-            }
-            *reinterpret_cast<v4f*>(&ps[(rp + 32 * i) * PS + 4 * c]) = pv;
-            rs += __shfl_xor(rs, 1);
-            rs += __shfl_xor(rs, 2);
-            rs += __shfl_xor(rs, 4);
-            alpha[i] = exp_e(m_prev[i] - mx);  // fa.cu:187
-            l[i] = fmaf(alpha[i], l[i], rs);  // fa.cu:190
-            m_prev[i] = mx;
-        }
-        __syncthreads();
-        // ---- O = alpha*O + P V (fa.cu:93-94,199): sequential fmaf chain over the tile's keys
-        float acc[2][CH][4] = {};
-#pragma unroll 2
-        for (int kv = 0; kv < 32; kv += 4) {
-            const v4f p0 = *reinterpret_cast<const v4f*>(&ps[rp * PS + kv]);
-            const v4f p1 = *reinterpret_cast<const v4f*>(&ps[(rp + 32) * PS + kv]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-#pragma unroll
-                for (int h = 0; h < CH; ++h) {
-                    const v4f vv = *reinterpret_cast<const v4f*>(&vs[(kv + e) * VS + 32 * h + 4 * c]);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[0][h][j] = fmaf(p0[e], vv[j], acc[0][h][j]);
-                        acc[1][h][j] = fmaf(p1[e], vv[j], acc[1][h][j]);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int h = 0; h < CH; ++h)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) o[i][h][j] = __fadd_rn(__fmul_rn(o[i][h][j], alpha[i]), acc[i][h][j]);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int row = row0 + rp + 32 * i;
-        if (row >= N) continue;
-        const bool ok = l[i] > 1e-10f;  // fa.cu:371
-        float* orow = O + head_off + (size_t)row * d_model;
-#pragma unroll
-        for (int h = 0; h < CH; ++h) {
-            v4f w;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = ok ? o[i][h][j] / l[i] : 0.0f;
-            *reinterpret_cast<v4f*>(orow + 32 * h + 4 * c) = w;
-        }
-    }
-}
-
-// v3: the v2 tiling generalised to RPT query rows per thread and NT threads (NT/8 * RPT rows per
-// workgroup).  RPT = 4 halves the LDS bytes per FMA of Q@K^T and P@V against v2's two rows (each
-// K / V / P vector read from LDS feeds RPT rows); the fmaf orders are v2's, so S is unchanged
-// bit for bit and O to the last ulp.
+// `fa`: the scalar kernel (VALU fmaf only, LDS tiling, no matrix cores -- BASELINE config 2 as
+// written, the reference's no-tensor-core comparison point, README.md:12).  One workgroup = NT
+// threads = NT/8 * RPT query rows of one (batch, head); thread (rp = tid / 8, c = tid % 8) owns
+// rows rp + (NT/8) i (i < RPT).  S phase: columns 4c..4c+3 of the 32-key tile, K kept
+// transposed in LDS so the four keys come in one ds_read_b128, Q read four k at a time; P@V
+// phase: output columns 32h + 4c .. +3.  Every K / V / P vector read from LDS feeds RPT rows
+// (RPT = 4: ~0.1 b128 reads per FMA).  Every S and P@V sum keeps the reference's sequential
+// fmaf order (fa.cu:63-86 under nvcc's default contraction; :93-94): S is bit-identical to the
+// oracle's, O differs only through exp.  K/V of tile t+1 are prefetched into registers while
+// tile t computes (fa.cu stages them through shared memory the same way, :300-330).
 template <int D, int RPT, int NT>
 __global__ __launch_bounds__(NT) void qmha_fa_f32_v3_kernel(const float* __restrict__ Q, const float* __restrict__ K,
                                                              const float* __restrict__ V, float* __restrict__ O, int N,
@@ -571,16 +329,6 @@ static hipError_t fa_f32_mfma(const float* Q, const float* K, const float* V, fl
     return hipGetLastError();
 }
 
-template <int D>
-static hipError_t fa_f32_v2(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
-                            hipStream_t stream) {
-    const int G = N / QMHA_GROUP;
-    const float inv_sqrt_d = 1.0f / sqrtf((float)D);  // fa.cu:410
-    hipLaunchKernelGGL((qmha_fa_f32_v2_kernel<D>), dim3(B * H * ((G + 1) / 2)), dim3(256), 0, stream, Q, K, V, O, N, H,
-                       d_model, inv_sqrt_d);
-    return hipGetLastError();
-}
-
 template <int D, int RPT, int NT>
 static hipError_t fa_f32_v3(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream) {
@@ -591,37 +339,32 @@ static hipError_t fa_f32_v3(const float* Q, const float* K, const float* V, floa
     return hipGetLastError();
 }
 
-template <int D>
-static hipError_t fa_f32_d(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int d_model,
-                           hipStream_t stream) {
-    const int G = N / QMHA_GROUP;
-    const float inv_sqrt_d = 1.0f / sqrtf((float)D);  // fa.cu:410
-    hipLaunchKernelGGL((qmha_fa_f32_kernel<D>), dim3(B * H * G), dim3(256), 0, stream, Q, K, V, O, N, H, d_model,
-                       inv_sqrt_d);
-    return hipGetLastError();
-}
-
 hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int D,
-                         int d_model, hipStream_t stream) {
-#ifdef QMHA_ABLATION  // tuning alternatives and the v1/v2 kernels at d = 64: profiling builds only
-    const int cfg = tune_config("QMHA_F32_CFG");
+                         int d_model, bool mfma, hipStream_t stream) {
+    if (mfma) {  // fa_mfma: v4 on the fp32 matrix cores (128 query rows per workgroup)
+        switch (D) {
+            case 32: return fa_f32_mfma<32>(Q, K, V, O, B, N, H, d_model, stream);
+            case 64: return fa_f32_mfma<64>(Q, K, V, O, B, N, H, d_model, stream);
+            case 128: return fa_f32_mfma<128>(Q, K, V, O, B, N, H, d_model, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
+#ifdef QMHA_ABLATION  // scalar-kernel geometry alternatives at d = 64: profiling builds only
     if (D == 64) {
-        switch (cfg) {
+        switch (tune_config("QMHA_F32_CFG")) {
             case 34: return fa_f32_v3<64, 4, 128>(Q, K, V, O, B, N, H, d_model, stream);
             case 36: return fa_f32_v3<64, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
             case 37: return fa_f32_v3<64, 2, 128>(Q, K, V, O, B, N, H, d_model, stream);
-            case 1: return fa_f32_d<64>(Q, K, V, O, B, N, H, d_model, stream);
-            case 2: return fa_f32_v2<64>(Q, K, V, O, B, N, H, d_model, stream);
-            case 3: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
             default: break;
         }
     }
 #endif
-    // every d: v4 on the fp32 matrix cores (128 query rows per workgroup)
+    // fa: the scalar kernel, 4 rows per thread (128 rows per workgroup; 64 at d = 128, whose
+    // Q / K / V / P tiles would otherwise take 121 KiB of LDS)
     switch (D) {
-        case 32: return fa_f32_mfma<32>(Q, K, V, O, B, N, H, d_model, stream);
-        case 64: return fa_f32_mfma<64>(Q, K, V, O, B, N, H, d_model, stream);
-        case 128: return fa_f32_mfma<128>(Q, K, V, O, B, N, H, d_model, stream);
+        case 32: return fa_f32_v3<32, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 64: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 128: return fa_f32_v3<128, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

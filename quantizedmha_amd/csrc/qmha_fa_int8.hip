@@ -996,24 +996,25 @@ __global__ __launch_bounds__(64) void qmha_debug_qk_int32_kernel(const int8_t* _
 // ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
-size_t int8_workspace_bytes(int B, int N, int H, int D) {
-    const size_t e = (size_t)B * H * N * D;
-    const size_t s = (size_t)B * H * (N / QMHA_GROUP) * sizeof(float);
-    return 2 * align_up(e, 256) + align_up(2 * e, 256) + 3 * align_up(s, 256);
+// Production layout: Ki, Vh, sK, sV (the main kernel quantises Q in registers).  with_q adds Qi
+// and sQ at the end for the int32 Q@K^T test hook, whose pre-pass quantises Q too.
+size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    return e + 2 * e + 2 * s + (with_q ? e + s : 0);
 }
 
-Int8Workspace int8_carve(void* ws, int B, int N, int H, int D) {
+Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
     Int8Workspace w;
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t e2 = align_up((size_t)B * H * N * D * 2, 256);
     const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
     char* p = static_cast<char*>(ws);
-    w.Qi = reinterpret_cast<int8_t*>(p);
-    w.Ki = reinterpret_cast<int8_t*>(p + e);
-    w.Vh = reinterpret_cast<_Float16*>(p + 2 * e);
-    w.sQ = reinterpret_cast<float*>(p + 2 * e + e2);
-    w.sK = reinterpret_cast<float*>(p + 2 * e + e2 + s);
-    w.sV = reinterpret_cast<float*>(p + 2 * e + e2 + 2 * s);
+    w.Ki = reinterpret_cast<int8_t*>(p);
+    w.Vh = reinterpret_cast<_Float16*>(p + e);
+    w.sK = reinterpret_cast<float*>(p + 3 * e);
+    w.sV = reinterpret_cast<float*>(p + 3 * e + s);
+    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s) : nullptr;
+    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s) : nullptr;
     return w;
 }
 

@@ -16,15 +16,15 @@ int tune_config(const char* env_name);
 
 // ---- INT8 (fa_tc_int8_b) ---------------------------------------------------------------
 struct Int8Workspace {
-    int8_t* Qi;  // [B*H][N][D]
+    int8_t* Qi;  // [B*H][N][D]  (test hook only: nullptr in the production carve)
     int8_t* Ki;  // [B*H][N][D]
     _Float16* Vh;  // [B*H][N/32][D][32]  quantised V as f16 integers (f16 operand slot order)
     float* sQ;   // [B*H][N/32]
     float* sK;
     float* sV;
 };
-size_t int8_workspace_bytes(int B, int N, int H, int D);
-Int8Workspace int8_carve(void* ws, int B, int N, int H, int D);
+size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
+Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
 // first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V;
 // num_tensors (default: all from first_tensor on) limits the roles launched (the standalone op)
@@ -58,9 +58,9 @@ hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, co
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,
                               hipStream_t stream);
 
-// ---- FP32 scalar (fa) ------------------------------------------------------------------
+// ---- FP32 (fa: scalar VALU kernel; fa_mfma: the same contract on v_mfma_f32_32x32x2_f32) -----
 hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* O, int B, int N, int H, int D,
-                         int d_model, hipStream_t stream);
+                         int d_model, bool mfma, hipStream_t stream);
 
 // ---- unfused 3-kernel baseline (unfused.cu) --------------------------------------------
 size_t unfused_workspace_bytes(int B, int N, int H, int D);

@@ -34,12 +34,15 @@ static Tensor flash_solve(const Tensor& Q, const Tensor& K, const Tensor& V, int
     auto Vc = V.contiguous();
     const int64_t q_elems = Qc.numel();
     TORCH_CHECK(d_model > 0 && q_elems % d_model == 0, "Q.numel() must be divisible by d_model");
-    TORCH_CHECK(Kc.numel() == q_elems && Vc.numel() == q_elems, "Q, K and V must have the same number of elements");
-    const int64_t B = Qc.dim() == 3 ? Qc.size(0) : 1;
-    const int64_t N = q_elems / d_model / B;
+    TORCH_CHECK(Kc.sizes() == Qc.sizes() && Vc.sizes() == Qc.sizes(), "Q, K and V must have the same shape");
+    // [B, N, d_model] is B sequences; any other layout is one sequence of numel / d_model rows,
+    // as in the reference (torch_ext.cpp:23-25), e.g. [N, h, d]
+    const bool batched = Qc.dim() == 3 && Qc.size(2) == d_model;
+    const int64_t B = batched ? Qc.size(0) : 1;
+    const int64_t N = batched ? Qc.size(1) : q_elems / d_model;
     int variant = qmha_variant_from_name(kernel.c_str());
     if (variant < 0) {
-        TORCH_WARN("Kernel selection supports fa, fa_tc_v1a, fa_tc_int8_b, unfused; '", kernel,
+        TORCH_WARN("Kernel selection supports fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma; '", kernel,
                    "' routing to default 'fa_tc_int8_b'");
         variant = QMHA_FA_TC_INT8_B;
     }

@@ -8,7 +8,8 @@ Same name, arguments, return value and error behaviour as the reference:
   * unknown kernel name   -> warning, routed to the default fa_tc_int8_b       (:32-34)
 Differences (additive): `kernel` really selects the variant (the reference only warned and
 used its build-time kernel); a 3-D input [B, N, d_model] is treated as B sequences (the
-reference has no batch); work is enqueued on torch's current stream instead of private
+reference has no batch; any other shape is one sequence of numel/d_model rows, as there); K and V
+must have Q's shape; work is enqueued on torch's current stream instead of private
 streams + a blocking sync (torch orders it with surrounding ops on that stream).
 ROCm tensors report device type 'cuda', exactly as the reference's is_cuda() check expects.
 """
@@ -22,10 +23,12 @@ from . import _lib
 
 
 def _shape(Q: torch.Tensor, d_model: int):
+    """(B, N): [B, N, d_model] is B sequences; any other layout is one sequence of
+    numel / d_model rows, as in the reference (torch_ext.cpp:23-25), e.g. [N, h, d]."""
     n = Q.numel()
-    if n % d_model != 0:
+    if d_model <= 0 or n % d_model != 0:
         raise RuntimeError("Q.numel() must be divisible by d_model")
-    if Q.dim() == 3:
+    if Q.dim() == 3 and Q.shape[2] == d_model:
         return Q.shape[0], Q.shape[1]
     return 1, n // d_model
 
@@ -41,8 +44,8 @@ def flash_solve(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int,
     Qc, Kc, Vc = Q.contiguous(), K.contiguous(), V.contiguous()
     d_model, num_heads = int(d_model), int(num_heads)
     B, N = _shape(Qc, d_model)
-    if Kc.numel() != Qc.numel() or Vc.numel() != Qc.numel():
-        raise RuntimeError("Q, K and V must have the same number of elements")
+    if Kc.shape != Qc.shape or Vc.shape != Qc.shape:
+        raise RuntimeError("Q, K and V must have the same shape")
     if kernel not in _lib.VARIANTS:
         warnings.warn(f"Kernel selection supports {sorted(_lib.VARIANTS)}; '{kernel}' routing to default "
                       f"'{_lib.DEFAULT_KERNEL}'")

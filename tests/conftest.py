@@ -12,6 +12,14 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 
 
+def pytest_terminal_summary(terminalreporter):
+    from tests import parity_log
+    if parity_log.ENTRIES:
+        terminalreporter.write_sep("-", "observed parity per case (GPU vs oracle)")
+        for line in parity_log.lines():
+            terminalreporter.write_line(line)
+
+
 @pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle

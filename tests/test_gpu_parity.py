@@ -3,13 +3,17 @@
 Tolerances (stated per SURVEY 8c; the oracle restates the reference algorithm, the GPU
 kernels deviate only in fp32 rounding order and the exp implementation):
   * int8: quantised Q/K/V bytes and scales, and int32 Q@K^T -> bit-exact
-          O vs oracle fa_int8: every element <= INT8_TOL_ORACLE (2e-3) abs and all but
-          INT8_FLIP_FRAC (0.2 %) of the elements <= INT8_TOL_TIGHT (5e-5) abs -- exp ulps can
-          flip one P rounding, which moves a row by sP*sV*|Vi|/l
+          O vs oracle fa_int8, bound by sequence length (int8_tol): an exp ulp can flip one
+          P rounding, which moves a row by sP*sV*|Vi|/l, and l grows with N:
+            N <= 256   every element <= 2e-3, all but 0.2 % <= 5e-5
+            N <  2048  every element <= 5e-4, all but 0.2 % <= 5e-5
+            N >= 2048  every element <= 1e-4, all but 0.2 % <= 5e-5 -- the
+                       BASELINE C4/C5 and reference-config cases
           O vs fp32 attention golden <= 5e-3 abs (quantisation error budget)
   * fp16: O vs oracle fa_fp16 <= 2e-4, vs golden within verify.cu's 1e-3 abs/rel
   * fp32: O vs oracle fa_fp32 <= 1e-5 abs
   * unfused: O vs cpu_attention <= 1e-5 abs
+The observed maximum of every case is printed in pytest's terminal summary (tests/parity_log.py).
 """
 import ctypes
 import os
@@ -18,6 +22,7 @@ import subprocess
 import numpy as np
 import pytest
 
+from tests import parity_log
 from tests.golden_io import load_case
 
 pytestmark = pytest.mark.gpu
@@ -27,14 +32,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # int8 vs oracle: the GPU's exp2 and the oracle's expf differ in the last ulp, which can move
 # p/sP across a .5 rounding boundary and change one Pi by 1.  One such flip moves O by
-# sP*sV*|Vi|/l (up to ~1e-3 at N=128), so the int8 check is statistical: every element within
-# INT8_TOL_ORACLE, and all but INT8_FLIP_FRAC of the elements within INT8_TOL_TIGHT.
-INT8_TOL_ORACLE = 2e-3
+# sP*sV*|Vi|/l (up to ~1e-3 at N=128, ~1e-5 at N=4096), so the int8 check is statistical: every
+# element within int8_tol(N), and all but INT8_FLIP_FRAC of the elements within INT8_TOL_TIGHT.
 INT8_TOL_TIGHT = 5e-5
 INT8_FLIP_FRAC = 2e-3
-TOL_ORACLE = {"fa_tc_int8_b": INT8_TOL_ORACLE, "fa_tc_v1a": 2e-4, "fa": 1e-5, "unfused": 1e-5}
-TOL_GOLDEN = {"fa_tc_int8_b": 5e-3, "fa_tc_v1a": 1e-3, "fa": 1e-5, "unfused": 1e-5}
+TOL_ORACLE = {"fa_tc_int8_b": 2e-3, "fa_tc_v1a": 2e-4, "fa": 1e-5, "fa_mfma": 1e-5, "unfused": 1e-5}
+TOL_GOLDEN = {"fa_tc_int8_b": 5e-3, "fa_tc_v1a": 1e-3, "fa": 1e-5, "fa_mfma": 1e-5, "unfused": 1e-5}
 VARIANTS = list(TOL_ORACLE)
+
+
+def int8_tol(N):
+    """Max |O_gpu - O_oracle| for fa_tc_int8_b at sequence length N (see the module docstring)."""
+    if N <= 256:
+        return 2e-3
+    if N < 2048:
+        return 5e-4
+    return 1e-4
 
 
 @pytest.fixture(scope="module")
@@ -50,12 +63,17 @@ def oracle_for(oracle_mod, variant):
     return oracle_mod.ORACLE_BY_VARIANT[variant]
 
 
-def assert_parity(variant, out, ref, scale=1.0):
+def assert_parity(variant, out, ref, scale=1.0, N=None):
+    """out/ref: [..., N, d_model]; N defaults to out.shape[-2] (the sequence length)."""
     err = np.abs(np.asarray(out, np.float64) - np.asarray(ref, np.float64))
     assert np.isfinite(out).all()
-    assert err.max() <= TOL_ORACLE[variant] * scale, (variant, float(err.max()))
+    n = int(N if N is not None else np.asarray(out).shape[-2])
+    tol = (int8_tol(n) if variant == "fa_tc_int8_b" else TOL_ORACLE[variant]) * scale
+    frac = float((err > INT8_TOL_TIGHT).mean())
+    parity_log.record(os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0].split("::")[-1], variant,
+                      err.max(), frac, tol)
+    assert err.max() <= tol, (variant, float(err.max()), tol)
     if variant == "fa_tc_int8_b":
-        frac = float((err > INT8_TOL_TIGHT).mean())
         assert frac <= INT8_FLIP_FRAC, (frac, float(err.max()))
 
 
@@ -412,17 +430,19 @@ def test_c3_fp16_full_config_sampled_heads(dev, oracle_mod):
     assert_parity("fa_tc_v1a", got, ref)
 
 
-def test_c2_fp32_full_config_all_heads(dev, oracle_mod):
-    """BASELINE C2 (fa, fp32 scalar, B8 H8 N1024 d64) at its own workload, every one of the 64
-    heads against oracle fa_fp32 at 1e-5 (fa.cu:211-400)."""
+@pytest.mark.parametrize("variant", ["fa", "fa_mfma"])
+def test_c2_fp32_full_config_all_heads(dev, oracle_mod, variant):
+    """BASELINE C2 (fa, fp32, B8 H8 N1024 d64) at its own workload, every one of the 64 heads
+    against oracle fa_fp32 at 1e-5 (fa.cu:211-400): the scalar no-matrix-core kernel the config
+    names (fa) and its fp32-MFMA sibling (fa_mfma)."""
     from quantizedmha_amd import torch_ext
     B, N, H, d = 8, 1024, 8, 64
     g = torch.Generator(device=dev).manual_seed(22)
     Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
-    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa")
+    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
     torch.cuda.synchronize()
     ref = oracle_mod.fa_fp32(Q.cpu().numpy(), K.cpu().numpy(), V.cpu().numpy(), H * d, H, 16)
-    assert_parity("fa", out.cpu().numpy(), ref)
+    assert_parity(variant, out.cpu().numpy(), ref)
 
 
 def test_compiled_torch_ext_module(dev, oracle_mod):
@@ -458,6 +478,22 @@ def test_compiled_torch_ext_module(dev, oracle_mod):
         warnings.simplefilter("always")
         c = compiled.flash_solve(Q, K, V, 256, 4, "fa_tc_v2b")  # unknown -> warned, default kernel
     assert torch.equal(c, mirror.flash_solve(Q, K, V, 256, 4))
+    # malformed 3-D shapes (round-2 ADVICE): both front-ends read a non-[B, N, d_model] 3-D tensor
+    # as ONE sequence of numel/d_model rows, like the reference, and reject mismatched K / V shapes
+    nhd = [x[1].reshape(256, 4, 64) for x in (Q, K, V)]  # [N, h, d]
+    for fe in (compiled.flash_solve, mirror.flash_solve):
+        r = fe(*nhd, 256, 4)
+        torch.cuda.synchronize()
+        assert r.shape == (256, 4, 64) and torch.equal(r.reshape(256, 256), two_d)
+        with pytest.raises(RuntimeError, match="same shape"):
+            fe(Q, K[:, :128], V, 256, 4)
+        with pytest.raises(RuntimeError, match="same shape"):
+            fe(Q[1].reshape(256, 4, 64), K[1], V[1], 256, 4)
+    small = Q[0, :64].reshape(32, 64, 8).contiguous()  # last dim != d_model: one sequence of 2 rows
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        compiled.flash_solve(small, small, small, 1024, 16)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        mirror.flash_solve(small, small, small, 1024, 16)
 
 
 def test_driver_binary_end_to_end(dev, tmp_path):

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Chunked pre-pass/main overlap must be bit-identical to the unchunked call: run the same
-inputs with QMHA_OVERLAP_CHUNKS=1 and =<n> in two subprocesses and compare."""
+inputs with 1 and 4 overlap chunks (qmha_set_overlap_chunks, set inside each child: the
+QMHA_OVERLAP_CHUNKS variable is read by QMHA_ABLATION builds only) in two subprocesses and
+compare.  Each child checks that the library accepted its chunk count."""
 import os
 import subprocess
 import sys
@@ -10,10 +12,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(B, N, H, d, variant, out):
+def child(B, N, H, d, variant, chunks, out):
     import torch
     sys.path.insert(0, ROOT)
-    from quantizedmha_amd import torch_ext
+    from quantizedmha_amd import _lib, torch_ext
+    lib = _lib.load()
+    lib.qmha_set_overlap_chunks(chunks)
+    assert lib.qmha_set_overlap_chunks(chunks) == chunks, "overlap chunk count not applied"
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
@@ -25,7 +30,7 @@ def child(B, N, H, d, variant, out):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
-        child(*map(int, sys.argv[2:6]), sys.argv[6], sys.argv[7])
+        child(*map(int, sys.argv[2:6]), sys.argv[6], int(sys.argv[7]), sys.argv[8])
         sys.exit(0)
     bad = 0
     shapes = ((16, 1024, 16, 64), (8, 512, 4, 64), (3, 256, 2, 128))
@@ -36,9 +41,8 @@ if __name__ == "__main__":
             res = []
             for chunks in (1, 4):
                 out = f"/tmp/ovl_{variant}_{B}_{chunks}.npy"
-                env = dict(os.environ, QMHA_OVERLAP_CHUNKS=str(chunks))
-                subprocess.run([sys.executable, __file__, "child", str(B), str(N), str(H), str(d), variant, out],
-                               env=env, check=True)
+                subprocess.run([sys.executable, __file__, "child", str(B), str(N), str(H), str(d), variant,
+                                str(chunks), out], check=True)
                 res.append(np.load(out))
             same = np.array_equal(res[0], res[1])
             diff = float(np.abs(res[0] - res[1]).max())
