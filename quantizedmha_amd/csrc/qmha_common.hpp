@@ -210,7 +210,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // column goes to this wave's LDS tile T (D rows of PITCH bytes) as 8-byte pieces; the tile is
 // read back in 8-byte pieces and stored to dst as whole 16-byte lines.
 // --------------------------------------------------------------------------
+// The 8-byte chunks of LDS row d are XOR-swizzled by (d >> 4) & 7: the 16 lanes of a ds_write_b64
+// lane group write 16 rows d = 4 c4 + c (stride 4 rows = 72 dwords = bank +8), which without the
+// swizzle hit only 4 bank pairs (4-way conflict; r02 PMC: SQ_LDS_BANK_CONFLICT 4.19 M of 6.29 M
+// LDS-active cycles in the int8 pre-pass); with it the writes are conflict-free for d = 32/64/128
+// (tools/lds_banks.py models both sides; the 8-byte read-back stays at its 2-way floor).
 constexpr int QMHA_VT_PITCH = 64 + 8;  // bytes per d-row of the LDS tile (8-byte pad)
+__device__ __forceinline__ int vt_chunk_swz(int d) { return (d >> 4) & 7; }
 template <int D, bool QUANT>
 __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
     constexpr int C4 = D / 4, NI = D / 8;
@@ -219,12 +225,13 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
     for (int c = 0; c < 4; ++c) {
         const int d = 4 * c4 + c;
 #pragma unroll
-        for (int a = 0; a < NI / 4; ++a) {  // kv rows NI rq + 4a .. +3 -> 4 consecutive slots
+        for (int a = 0; a < NI / 4; ++a) {  // kv rows NI rq + 4a .. +3 -> 4 consecutive slots (one 8-byte chunk)
             v4h h;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
                 h[e] = QUANT ? (_Float16)qmha_quant_i8(x[4 * a + e][c], inv) : (_Float16)x[4 * a + e][c];
-            *reinterpret_cast<v4h*>(T + d * QMHA_VT_PITCH + 2 * slot_of_kv_f16(NI * rq + 4 * a)) = h;
+            const int chunk = slot_of_kv_f16(NI * rq + 4 * a) >> 2;
+            *reinterpret_cast<v4h*>(T + d * QMHA_VT_PITCH + 8 * (chunk ^ vt_chunk_swz(d))) = h;
         }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
@@ -233,8 +240,8 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
 #pragma unroll
     for (int u = lane; u < LINES; u += 64) {
         const int d = u >> 2, q = u & 3;
-        const v2i lo = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 16 * q);
-        const v2i hi = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 16 * q + 8);
+        const v2i lo = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q) ^ vt_chunk_swz(d)));
+        const v2i hi = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q + 1) ^ vt_chunk_swz(d)));
         *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
     }
 }

@@ -4,10 +4,11 @@ Every (sequence, head) pair of the attention forward is independent, so the mult
 a pure partition of the batch: rank r of W owns sequences [start_r, stop_r) and runs the
 single-GPU kernel on them with no data-path collective.  The north star's RCCL all-gather of
 the per-shard outputs over xGMI is a separate, optional step; outputs are batch-outermost
-[B, N, d_model], so every rank's shard is one contiguous slab of the result.  With
-`chunks > 1` the shard is computed in batch chunks and the all-gather of chunk c runs on the
-collective's own stream while chunk c+1 is being computed (the gather is ~1/3 of the compute
-at C5 over one xGMI link per peer, so only the last chunk's gather is exposed).
+[B, N, d_model], so every rank's shard is one contiguous slab of the result: each rank's
+kernels write their rows straight into the result tensor and the gather is a point-to-point
+exchange into the peers' slabs (no staging buffer, no reorder copy).  With `chunks > 1` the
+shard is computed in batch chunks and the exchange of chunk c runs on the collective's own
+stream while chunk c+1 is being computed.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm; "gloo" for CPU tests).
 Each rank only ever holds its own shard of Q/K/V (`batch=` form of `solve_sharded`), so the
@@ -69,47 +70,70 @@ def gather_outputs(O_local: torch.Tensor, batch: int, group=None) -> torch.Tenso
 
 def solve_shard_gather(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int,
                        batch: int, kernel: str = "fa_tc_int8_b", group=None, chunks: int = 1,
-                       solve_fn: Optional[Callable] = None) -> torch.Tensor:
+                       solve_fn: Optional[Callable] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """This rank's shard [b_r, N, d_model] in; the full [batch, N, d_model] out on every rank.
 
-    The shard is computed in `chunks` batch chunks; chunk c's all-gather is issued
-    asynchronously right after its compute is enqueued, so it overlaps chunk c+1's kernels
-    (RCCL orders it after chunk c on the compute stream by itself).  Chunk boundaries are the
-    same on every rank (chunks of the padded shard width), so each collective moves equal
-    sizes; a rank with a short shard contributes zero padding that is trimmed at the end."""
+    Copy-free: the result tensor `out` is allocated once (or passed in) and every rank's kernels
+    write their rows straight into their own slab of it (flash_solve(out=...)).  The exchange is
+    point-to-point: for each batch chunk c, every rank sends its chunk-c rows to each peer and
+    receives each peer's chunk-c rows straight into that peer's slab (one isend / irecv pair per
+    peer, batched in one RCCL group).  On the MI355X node's xGMI full mesh every peer's data
+    travels on its own link, and nothing is staged, padded or reordered: uneven shards just send
+    fewer rows.  Chunk c's exchange is issued right after chunk c's kernels are enqueued, so it
+    runs on the collective stream while chunk c+1 computes; chunk boundaries (chunks of the
+    largest shard's width) are the same on every rank, so sends and receives pair up.
+
+    solve_fn (CPU tests: the oracle) returns a new tensor that is copied into the slab; the
+    default HIP path writes in place."""
     world, rank = _world(group)
     lo, hi = batch_shard(batch, rank, world)
     if Q.shape[0] != hi - lo:
         raise ValueError(f"rank {rank} of {world}: expected its shard of {hi - lo} sequences, got {Q.shape[0]}")
-    if solve_fn is None:
-        from .torch_ext import flash_solve as solve_fn  # HIP path; raises if the library is absent
-    width = max(stop - start for start, stop in (batch_shard(batch, r, world) for r in range(world)))
+    if out is None:
+        out = Q.new_empty((batch,) + tuple(Q.shape[1:]))
+    elif out.shape != (batch,) + tuple(Q.shape[1:]) or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous {(batch,) + tuple(Q.shape[1:])} tensor")
+
+    def compute(q, k, v, dst):
+        if solve_fn is None:
+            from .torch_ext import flash_solve  # HIP path; raises if the library is absent
+            flash_solve(q, k, v, d_model, num_heads, kernel, out=dst)
+        else:
+            dst.copy_(solve_fn(q, k, v, d_model, num_heads, kernel))
+
     if world == 1:
-        return solve_fn(Q, K, V, d_model, num_heads, kernel)
+        compute(Q, K, V, out)
+        return out
+    sizes = [batch_shard(batch, r, world) for r in range(world)]
+    width = max(stop - start for start, stop in sizes)
     C = max(1, min(int(chunks), width))
-    buf = Q.new_empty((world * width,) + tuple(Q.shape[1:]))
     works: List = []
-    keep: List[torch.Tensor] = []
     for c in range(C):
         c0, c1 = batch_shard(width, c, C)
-        n = max(0, min(c1, Q.shape[0]) - c0)
+        n = max(0, min(c1, hi - lo) - c0)
+        mine = out[lo + c0:lo + c0 + n]
         if n > 0:
-            O_c = solve_fn(Q[c0:c0 + n], K[c0:c0 + n], V[c0:c0 + n], d_model, num_heads, kernel)
-        else:
-            O_c = Q.new_empty((0,) + tuple(Q.shape[1:]))
-        O_c = _padded(O_c, c1 - c0)
-        views = [buf[r * width + c0:r * width + c1] for r in range(world)]
-        works.append(dist.all_gather(views, O_c, group=group, async_op=True))
-        keep.append(O_c)
+            compute(Q[c0:c0 + n], K[c0:c0 + n], V[c0:c0 + n], mine)
+        ops = []
+        for p, (ps, pe) in enumerate(sizes):
+            if p == rank:
+                continue
+            if n > 0:
+                ops.append(dist.P2POp(dist.isend, mine, p, group))
+            n_p = max(0, min(c1, pe - ps) - c0)
+            if n_p > 0:
+                ops.append(dist.P2POp(dist.irecv, out[ps + c0:ps + c0 + n_p], p, group))
+        if ops:
+            works.extend(dist.batch_isend_irecv(ops))
     for w in works:
         w.wait()
-    return _trim(buf, batch, world, width)
+    return out
 
 
 def solve_sharded(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int,
                   kernel: str = "fa_tc_int8_b", gather: bool = True, group=None,
                   solve_fn: Optional[Callable] = None, batch: Optional[int] = None,
-                  chunks: int = 1) -> torch.Tensor:
+                  chunks: int = 1, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Batch-sharded attention forward.
 
     batch=None: Q, K, V are the FULL batch [B, N, d_model] (or views of it) and rank r slices
@@ -117,7 +141,8 @@ def solve_sharded(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: in
     is how a real C5 job holds its inputs (no rank ever materialises the global batch).
     Rank r computes its shard with `solve_fn` (default: torch_ext.flash_solve, the HIP
     kernels) and, if `gather`, returns the full [B, N, d_model] output on every rank
-    (all-gather overlapped with compute when chunks > 1), else its own shard.
+    (point-to-point exchange overlapped with compute when chunks > 1; written into `out` when
+    given), else its own shard.
     """
     if Q.dim() != 3:
         raise ValueError("solve_sharded expects [B, N, d_model] inputs")
@@ -133,4 +158,4 @@ def solve_sharded(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: in
         if Q.shape[0] != hi - lo:
             raise ValueError(f"rank {rank} of {world}: expected its shard of {hi - lo} sequences, got {Q.shape[0]}")
         return solve_fn(Q, K, V, d_model, num_heads, kernel)
-    return solve_shard_gather(Q, K, V, d_model, num_heads, batch, kernel, group, chunks, solve_fn)
+    return solve_shard_gather(Q, K, V, d_model, num_heads, batch, kernel, group, chunks, solve_fn, out)

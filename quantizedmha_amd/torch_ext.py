@@ -16,6 +16,7 @@ ROCm tensors report device type 'cuda', exactly as the reference's is_cuda() che
 from __future__ import annotations
 
 import warnings
+from typing import Optional
 
 import torch
 
@@ -34,8 +35,10 @@ def _shape(Q: torch.Tensor, d_model: int):
 
 
 def flash_solve(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int,
-                kernel: str = _lib.DEFAULT_KERNEL) -> torch.Tensor:
-    """FlashAttention solve (HIP).  Q, K, V: [N, d_model] (or [B, N, d_model]) fp32 on the GPU."""
+                kernel: str = _lib.DEFAULT_KERNEL, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FlashAttention solve (HIP).  Q, K, V: [N, d_model] (or [B, N, d_model]) fp32 on the GPU.
+    out (additive): a contiguous fp32 tensor of Q's shape on Q's device to write the result into
+    (the batch-shard path writes each rank's rows straight into the gathered result)."""
     if not (Q.is_cuda and K.is_cuda and V.is_cuda):
         raise RuntimeError("Inputs must be CUDA tensors")
     for name, t in (("Q", Q), ("K", K), ("V", V)):
@@ -50,7 +53,11 @@ def flash_solve(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int,
         warnings.warn(f"Kernel selection supports {sorted(_lib.VARIANTS)}; '{kernel}' routing to default "
                       f"'{_lib.DEFAULT_KERNEL}'")
         kernel = _lib.DEFAULT_KERNEL
-    out = torch.empty_like(Qc)
+    if out is None:
+        out = torch.empty_like(Qc)
+    elif (out.shape != Qc.shape or out.dtype != torch.float32 or out.device != Qc.device
+          or not out.is_contiguous()):
+        raise RuntimeError("out must be a contiguous float32 tensor of Q's shape on Q's device")
     lib = _lib.load()
     with torch.cuda.device(Qc.device):
         stream = torch.cuda.current_stream(Qc.device).cuda_stream

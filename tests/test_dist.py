@@ -61,6 +61,14 @@ def _worker(rank, world, port, B, kernel, result_path):
         assert torch.equal(mine, local)
         with pytest.raises(ValueError):  # a shard of the wrong size is refused, not mis-gathered
             solve_sharded(Q, K, V, 128, 2, kernel, batch=B, solve_fn=_oracle_solve(oracle))
+        # the result is written in place (no staging copy): a caller-provided buffer comes back
+        buf = torch.empty(B, 64, 128)
+        res = solve_sharded(*sh, 128, 2, kernel, batch=B, chunks=3, solve_fn=_oracle_solve(oracle), out=buf)
+        assert res.data_ptr() == buf.data_ptr() and torch.equal(res, outs[3])
+        # every rank holds the same gathered result: compare against rank 0's through a broadcast
+        ref0 = out.clone()
+        dist.broadcast(ref0, 0)
+        assert torch.equal(ref0, out)
         if rank == 0:
             torch.save({"out": out, **{f"chunked{c}": o for c, o in outs.items()}}, result_path)
     finally:
@@ -73,10 +81,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("B,kernel", [(4, "fa_tc_int8_b"), (3, "fa")])
-def test_shard_gloo_world2(oracle_mod, tmp_path, B, kernel):
+@pytest.mark.parametrize("world,B,kernel", [(2, 4, "fa_tc_int8_b"), (2, 3, "fa"), (4, 7, "fa_tc_int8_b"),
+                                            (4, 10, "fa_tc_v1a")])
+def test_shard_gloo(oracle_mod, tmp_path, world, B, kernel):
+    """world 2 and 4, even and uneven shards (B = 7 over 4 ranks: 2, 2, 2, 1; B = 10: 3, 3, 2, 2),
+    1 / 2 / 3 chunks: every rank's gathered result equals the unsharded computation exactly."""
     path = str(tmp_path / "out.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), B, kernel, path), nprocs=2, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), B, kernel, path), nprocs=world, join=True,
                        start_method="spawn")
     res = torch.load(path, weights_only=True)
     Q, K, V = _inputs(B, 64, 128)
