@@ -214,7 +214,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
        FL_DUMP = 256, FL_PIN = 512,
        FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
-       FL_DMA_SPLIT = 16384, FL_RING4 = 32768 };
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -623,7 +623,16 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
     constexpr int kOps32[3] = {0, 1, 1000};  // PV00 PV01 QK0
     constexpr int kSlot128[6] = {2, 2, 2, 2, 2, 2};
-    constexpr int kOps128[12] = {0, 2, 4, 6, 1000, 1001, 1, 3, 5, 7, 1002, 1003};
+#ifndef QMHA_D128_SCHED
+#define QMHA_D128_SCHED 1
+#endif
+    // d = 128 (QMHA_D128_SCHED 1): A PV00 PV10 | B PV20 QK0 | C PV30 PV01 | D QK1 PV11 | E PV21 QK2 |
+    // F PV31 QK3 -- every chained pair (PV(m,0) -> PV(m,1), QK(k) -> QK(k+1)) is separated by a VALU
+    // chunk and another MFMA (round-2 ADVICE: the r02 table, QMHA_D128_SCHED 0, issued QK0 -> QK1 and
+    // QK2 -> QK3 back to back)
+    constexpr int kOps128[12] = {0, 2, 4, QMHA_D128_SCHED ? 1000 : 6, QMHA_D128_SCHED ? 6 : 1000,
+                                 QMHA_D128_SCHED ? 1 : 1001, QMHA_D128_SCHED ? 1001 : 1, 3, 5,
+                                 QMHA_D128_SCHED ? 1002 : 7, QMHA_D128_SCHED ? 7 : 1002, 1003};
     auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
     auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]); };
     static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
@@ -641,8 +650,16 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // operands and result live, so the rest of the loop compiles to the same VALU work / no
     // LDS-DMA issued (barriers and operand reads unchanged)
     constexpr bool NOMFMA = FL & FL_ABL_NOMFMA, NOEXP = FL & FL_ABL_NOEXP;
+    // FL_ABL_NOMFMA2 (r03): the same without a single added instruction -- the Q@K^T "result"
+    // keeps the prologue's bias-only block (S = 0: sane scores, no re-anchoring), each P@V
+    // "result" is a fresh undefined register block (ks = 0) or the previous one (ks = 1), so the
+    // compiled VALU / LDS / DMA stream equals the real kernel's minus the MFMAs
+    constexpr bool NOMFMA2 = FL & FL_ABL_NOMFMA2;
+    if constexpr (NOMFMA2) s_nxt = magic_blk;
     auto qk = [&](const v4i& kk, int ks) {
-        if constexpr (NOMFMA) {
+        if constexpr (NOMFMA2) {
+            asm volatile("" : "+v"(s_nxt) : "v"(kk), "v"(qop[ks]));
+        } else if constexpr (NOMFMA) {
             if (ks == 0) s_nxt = magic_blk;
             asm volatile("" : "+v"(s_nxt) : "v"(kk), "v"(qop[ks]));
         } else {
@@ -786,7 +803,12 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                     } else {
                         const int m = op >> 1, ks = op & 1;
                         if (has_prev) {
-                            if constexpr (NOMFMA) {
+                            if constexpr (NOMFMA2) {
+                                if (ks == 0)
+                                    asm volatile("" : "=v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                                else
+                                    asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                            } else if constexpr (NOMFMA) {
                                 if (ks == 0) a[m] = v16f{};
                                 asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
                             } else {
@@ -1106,6 +1128,8 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, Qf, O, B, N, H, d_model, stream);
             case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, Qf, O, B, N, H, d_model, stream);
             case 11000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 10000>(w, Qf, O, B, N, H, d_model, stream);
+            case 14000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ABL_NOMFMA2>(w, Qf, O, B, N, H, d_model, stream);
+            case 15000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ABL_NOEXP>(w, Qf, O, B, N, H, d_model, stream);
             case 12000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 20000>(w, Qf, O, B, N, H, d_model, stream);
             case 13000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 30000>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
