@@ -6,7 +6,7 @@
 //   P stored as half(p) (:174);  O = alpha*O + Ph Vh (fp32 accumulate, :218)
 //   out = O / l, 0 if l <= 1e-10 (:384-388)
 //
-// Same skeleton as the INT8 kernel: a conversion pre-pass writes K as f16 rows and V in the
+// Same skeleton as the INT8 kernel: a conversion pre-pass (qmha_prepass.hip) writes K as f16 rows and V in the
 // f16 V^T operand order; the main kernel converts its Q group into registers, streams K/V
 // tiles through LDS-DMA-filled swizzled LDS and runs both products on
 // v_mfma_f32_32x32x16_f16 with swapped operands.  The O accumulator is the MFMA C operand,
@@ -19,56 +19,6 @@
 namespace qmha {
 
 static constexpr float kLog2eH = 1.4426950408889634f;
-
-template <int D>
-__global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
-    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-    _Float16* __restrict__ Qh, _Float16* __restrict__ Kh, _Float16* __restrict__ Vt,
-    int N, int H, int d_model, int total_groups, int first_tensor) {
-    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
-    const int tensor = blockIdx.y + first_tensor;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int item = blockIdx.x * 4 + wave;
-    const bool active = item < total_groups;
-    const int G = N / QMHA_GROUP;
-    const int bh = active ? item / G : 0, g = active ? item % G : 0;
-    const int b = bh / H, k = bh % H;
-    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
-    if (tensor == 2) {
-        // V^T operand order through a per-wave LDS transpose (vt_group_store, shared with the
-        // int8 pre-pass): coalesced 16-byte non-temporal loads of NI consecutive rows per lane
-        __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
-        if (active) {
-            const int rq = lane / C4, c4 = lane % C4;
-            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
-            v4f x[NI];
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-                x[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
-            vt_group_store<D, false>(vtr[wave], x, 1.0f, lane,
-                                     reinterpret_cast<char*>(Vt + ((size_t)bh * G + g) * (size_t)(32 * D)));
-        }
-        return;
-    }
-    const int ri = lane / C4, ci = lane % C4;
-    v4f v[NI];
-    if (active) {
-        const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
-    }
-    if (active) {  // Q, K: f16 rows
-        _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            v4h hv;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)
-            *reinterpret_cast<v4h*>(dst + (size_t)(i * RPI + ri) * D) = hv;
-        }
-    }
-}
 
 template <int RB>
 __device__ __forceinline__ int chunk_swz_h(int row) {
@@ -337,26 +287,6 @@ F16Workspace f16_carve(void* ws, int B, int N, int H, int D) {
     w.Kh = reinterpret_cast<_Float16*>(p);
     w.Vt = reinterpret_cast<_Float16*>(p + e);
     return w;
-}
-
-template <int D>
-static hipError_t convert_f16_d(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
-                                int H, int d_model, hipStream_t stream) {
-    const int total = B * H * (N / QMHA_GROUP);
-    // K and V only: the main kernel converts Q itself (blockIdx.y = tensor - 1)
-    hipLaunchKernelGGL((qmha_convert_f16_kernel<D>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V, w.Qh,
-                       w.Kh, w.Vt, N, H, d_model, total, 1);
-    return hipGetLastError();
-}
-
-hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
-                              int H, int D, int d_model, hipStream_t stream) {
-    switch (D) {
-        case 32: return convert_f16_d<32>(Q, K, V, w, B, N, H, d_model, stream);
-        case 64: return convert_f16_d<64>(Q, K, V, w, B, N, H, d_model, stream);
-        case 128: return convert_f16_d<128>(Q, K, V, w, B, N, H, d_model, stream);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 template <int D, int WAVES, int SG, int FL>

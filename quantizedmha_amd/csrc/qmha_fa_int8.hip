@@ -9,7 +9,7 @@
 //   O = alpha*O + (Pi Vi) * sP * sV,   out = O / l  (0 if l <= 1e-20)
 //
 // Two launches per call:
-//   1. qmha_quant_int8_kernel: reads fp32 K/V once; writes int8 K rows per head and the
+//   1. qmha_quant_int8_kernel (qmha_prepass.hip): reads fp32 K/V once; writes int8 K rows per head and the
 //      quantised V integers in the MFMA V^T operand order, one fp32 scale per group.
 //      Bit-identical to the reference quantiser (same fp32 ops, RNE rounding).  (With Q too
 //      for qmha_quantize_int8 and the int32 Q@K^T test hook.)
@@ -37,110 +37,6 @@ namespace qmha {
 
 // log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
 static constexpr float kLog2e = 1.4426950408889634f;
-
-#ifndef QMHA_PRE_NT
-#define QMHA_PRE_NT 1
-#endif
-#if QMHA_PRE_NT
-#define QMHA_PRE_LOAD(p) __builtin_nontemporal_load(p)
-#else
-#define QMHA_PRE_LOAD(p) (*(p))
-#endif
-// ---------------------------------------------------------------------------------------
-// Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
-// One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
-// v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
-// v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
-// ---------------------------------------------------------------------------------------
-// One wave quantises one 32-row group of V (b, k, g) into the V^T operand order through its
-// LDS tile `vtr` (D * QMHA_VT_PITCH bytes): coalesced 16-byte loads (instruction i covers rows
-// i, NI+i, ...: 256-byte row segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns
-// 4 c4..4 c4+3.  In the slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots
-// (kv_of_slot_f16), so each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile
-// is read back in 8-byte pieces and stored as 16-byte lines.  Loads are non-temporal: fp32
-// K/V are read exactly once per call.
-// v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
-// v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
-template <int D, int VMODE>
-__device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void* __restrict__ Vout,
-                                              float* __restrict__ sV, char* vtr, int lane, int b, int k, int g,
-                                              int bh, int N, int G, int d_model) {
-    constexpr int C4 = D / 4, NI = 32 / (64 / C4);
-    const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
-    v4f x[NI];
-    float amax = 0.0f;
-    const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
-    }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);
-    const float inv = 1.0f / sc;
-    if constexpr (VMODE == 1)
-        vt_group_store<D, true>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
-    else
-        vt8_group_store<D>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
-    if (lane == 0) sV[(size_t)bh * G + g] = sc;
-}
-
-// One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
-template <int D>
-__device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int8_t* __restrict__ Xi,
-                                                float* __restrict__ sX, int lane, int b, int k, int g, int bh, int N,
-                                                int G, int d_model) {
-    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
-    const int ri = lane / C4, ci = lane % C4;
-    v4f v[NI];
-    float amax = 0.0f;
-    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        v[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
-    }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);  // :104
-    const float inv = 1.0f / sc;                     // :106 (correctly rounded division)
-    int8_t* dst = Xi + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
-        *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
-    }
-    if (lane == 0) sX[(size_t)bh * G + g] = sc;
-}
-
-// ---------------------------------------------------------------------------------------
-// Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
-// One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
-// ---------------------------------------------------------------------------------------
-template <int D, int VMODE>
-__global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
-    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-    int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
-    float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int first_tensor) {
-    __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
-    const int tensor = blockIdx.y + first_tensor;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int item = blockIdx.x * 4 + wave;  // (bh, g)
-    if (item >= total_groups) return;        // wave-uniform
-    const int G = N / QMHA_GROUP;
-    const int bh = item / G, g = item % G;
-    const int b = bh / H, k = bh % H;
-    if (tensor == 2)
-        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
-    else
-        quant_row_group<D>(tensor == 0 ? Q : K, tensor == 0 ? Qi : Ki, tensor == 0 ? sQ : sK, lane, b, k, g, bh, N, G,
-                           d_model);
-}
 
 // LDS XOR swizzle for a row of RB bytes read as 16-byte chunks by ds_read_b128 with one
 // row per lane (rows 0..31 of a 32x32 operand): conflict-free per 16-lane group.
@@ -1038,34 +934,6 @@ Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
     w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s) : nullptr;
     w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s) : nullptr;
     return w;
-}
-
-template <int D>
-static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                               int v_mode, int B, int N, int H, int d_model, int first_tensor, int num_tensors,
-                               hipStream_t stream) {
-    const int total = B * H * (N / QMHA_GROUP);
-    dim3 grid((total + 3) / 4, num_tensors > 0 ? num_tensors : 3 - first_tensor);
-    if (v_mode == 0)
-        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 0>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
-                           w.sK, w.sV, N, H, d_model, total, first_tensor);
-    else
-        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
-                           w.sK, w.sV, N, H, d_model, total, first_tensor);
-    return hipGetLastError();
-}
-
-hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
-                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream, int first_tensor,
-                             int num_tensors) {
-    if (first_tensor < 0 || first_tensor > 2 || (num_tensors > 0 && first_tensor + num_tensors > 3))
-        return hipErrorInvalidValue;
-    switch (D) {
-        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
-        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
-        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL = 0>

@@ -1,0 +1,218 @@
+// qmha_prepass.hip -- the K/V pre-passes of the int8 and fp16 paths (and the standalone
+// qmha_quantize_int8 op), in a translation unit of their own: they read the caller's Q/K/V, so they
+// keep IEEE NaN semantics (the main-kernel sources are built with -fno-honor-nans, round-2 ADVICE).
+//   qmha_quant_int8_kernel  fa_tc_int8_b.cu:33-152 (fp32_to_int8sram): per 32-row group of every
+//                           head, sc = max(absmax/127, 1e-8), x_i8 = clamp(rint(x * (1/sc))) --
+//                           K as int8 rows, V as f16-valued integers in the MFMA V^T operand order
+//   qmha_convert_f16_kernel fa_tc_v1a.cu:300-330: K as f16 rows, V in the f16 V^T operand order (RNE)
+#include "qmha_common.hpp"
+#include "qmha_kernels.hpp"
+
+namespace qmha {
+
+#ifndef QMHA_PRE_NT
+#define QMHA_PRE_NT 1
+#endif
+#if QMHA_PRE_NT
+#define QMHA_PRE_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define QMHA_PRE_LOAD(p) (*(p))
+#endif
+// ---------------------------------------------------------------------------------------
+// Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
+// One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
+// v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
+// v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
+// ---------------------------------------------------------------------------------------
+// One wave quantises one 32-row group of V (b, k, g) into the V^T operand order through its
+// LDS tile `vtr` (D * QMHA_VT_PITCH bytes): coalesced 16-byte loads (instruction i covers rows
+// i, NI+i, ...: 256-byte row segments), so lane (rq, c4) holds NI CONSECUTIVE rows of columns
+// 4 c4..4 c4+3.  In the slot order consecutive kv rows 4a..4a+3 are 4 consecutive slots
+// (kv_of_slot_f16), so each column of the lane is 8-byte ds_write_b64 pieces; the [d][32] tile
+// is read back in 8-byte pieces and stored as 16-byte lines.  Loads are non-temporal: fp32
+// K/V are read exactly once per call.
+// v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
+// v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
+template <int D, int VMODE>
+__device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void* __restrict__ Vout,
+                                              float* __restrict__ sV, char* vtr, int lane, int b, int k, int g,
+                                              int bh, int N, int G, int d_model) {
+    constexpr int C4 = D / 4, NI = 32 / (64 / C4);
+    const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
+    v4f x[NI];
+    float amax = 0.0f;
+    const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
+    }
+    amax = wave_max64(amax);
+    const float sc = qmha_scale_from_absmax(amax);
+    const float inv = 1.0f / sc;
+    if constexpr (VMODE == 1)
+        vt_group_store<D, true>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
+    else
+        vt8_group_store<D>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
+    if (lane == 0) sV[(size_t)bh * G + g] = sc;
+}
+
+// One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
+template <int D>
+__device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int8_t* __restrict__ Xi,
+                                                float* __restrict__ sX, int lane, int b, int k, int g, int bh, int N,
+                                                int G, int d_model) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
+    const int ri = lane / C4, ci = lane % C4;
+    v4f v[NI];
+    float amax = 0.0f;
+    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        v[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
+    }
+    amax = wave_max64(amax);
+    const float sc = qmha_scale_from_absmax(amax);  // :104
+    const float inv = 1.0f / sc;                     // :106 (correctly rounded division)
+    int8_t* dst = Xi + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
+        *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
+    }
+    if (lane == 0) sX[(size_t)bh * G + g] = sc;
+}
+
+// ---------------------------------------------------------------------------------------
+// Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
+// One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
+// ---------------------------------------------------------------------------------------
+template <int D, int VMODE>
+__global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+    int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
+    float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
+    int N, int H, int d_model, int total_groups, int first_tensor) {
+    __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
+    const int tensor = blockIdx.y + first_tensor;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + wave;  // (bh, g)
+    if (item >= total_groups) return;        // wave-uniform
+    const int G = N / QMHA_GROUP;
+    const int bh = item / G, g = item % G;
+    const int b = bh / H, k = bh % H;
+    if (tensor == 2)
+        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
+    else
+        quant_row_group<D>(tensor == 0 ? Q : K, tensor == 0 ? Qi : Ki, tensor == 0 ? sQ : sK, lane, b, k, g, bh, N, G,
+                           d_model);
+}
+
+
+template <int D>
+__global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+    _Float16* __restrict__ Qh, _Float16* __restrict__ Kh, _Float16* __restrict__ Vt,
+    int N, int H, int d_model, int total_groups, int first_tensor) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
+    const int tensor = blockIdx.y + first_tensor;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + wave;
+    const bool active = item < total_groups;
+    const int G = N / QMHA_GROUP;
+    const int bh = active ? item / G : 0, g = active ? item % G : 0;
+    const int b = bh / H, k = bh % H;
+    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
+    if (tensor == 2) {
+        // V^T operand order through a per-wave LDS transpose (vt_group_store, shared with the
+        // int8 pre-pass): coalesced 16-byte non-temporal loads of NI consecutive rows per lane
+        __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
+        if (active) {
+            const int rq = lane / C4, c4 = lane % C4;
+            const float* base = V + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * c4;
+            v4f x[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                x[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(NI * rq + i) * d_model));
+            vt_group_store<D, false>(vtr[wave], x, 1.0f, lane,
+                                     reinterpret_cast<char*>(Vt + ((size_t)bh * G + g) * (size_t)(32 * D)));
+        }
+        return;
+    }
+    const int ri = lane / C4, ci = lane % C4;
+    v4f v[NI];
+    if (active) {
+        const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
+    }
+    if (active) {  // Q, K: f16 rows
+        _Float16* dst = (tensor == 0 ? Qh : Kh) + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            v4h hv;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) hv[c] = (_Float16)v[i][c];  // RNE (= __float2half)
+            *reinterpret_cast<v4h*>(dst + (size_t)(i * RPI + ri) * D) = hv;
+        }
+    }
+}
+
+
+template <int D>
+static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
+                               int v_mode, int B, int N, int H, int d_model, int first_tensor, int num_tensors,
+                               hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    dim3 grid((total + 3) / 4, num_tensors > 0 ? num_tensors : 3 - first_tensor);
+    if (v_mode == 0)
+        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 0>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
+                           w.sK, w.sV, N, H, d_model, total, first_tensor);
+    else
+        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
+                           w.sK, w.sV, N, H, d_model, total, first_tensor);
+    return hipGetLastError();
+}
+
+hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
+                             int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream, int first_tensor,
+                             int num_tensors) {
+    if (first_tensor < 0 || first_tensor > 2 || (num_tensors > 0 && first_tensor + num_tensors > 3))
+        return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+        case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+        case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+
+template <int D>
+static hipError_t convert_f16_d(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
+                                int H, int d_model, hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    // K and V only: the main kernel converts Q itself (blockIdx.y = tensor - 1)
+    hipLaunchKernelGGL((qmha_convert_f16_kernel<D>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V, w.Qh,
+                       w.Kh, w.Vt, N, H, d_model, total, 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
+                              int H, int D, int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return convert_f16_d<32>(Q, K, V, w, B, N, H, d_model, stream);
+        case 64: return convert_f16_d<64>(Q, K, V, w, B, N, H, d_model, stream);
+        case 128: return convert_f16_d<128>(Q, K, V, w, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace qmha

@@ -27,7 +27,8 @@ BIN = os.path.join(ROOT, "quantizedmha_amd", "bin")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_fa_f32.hip", "qmha_unfused.hip", "qmha_api.cpp"]
+KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_prepass.hip", "qmha_fa_f32.hip", "qmha_unfused.hip",
+                  "qmha_api.cpp"]
 VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4}
 DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
 HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
@@ -65,7 +66,8 @@ def header_deps():
 # per-source flags: the int8 softmax is written as scalar fp32 chains on purpose; SLP-packing
 # them into v_pk_* needs register pairs the exp results do not land in (a v_mov per pair)
 # -fno-honor-nans: fmaxf on MFMA results and running maxima otherwise gets a canonicalising
-# v_max (x, x) in front of it (5 per fp16 tile; scores here are finite by construction)
+# v_max (x, x) in front of it (5 per fp16 tile); the main kernels only.  The pre-passes that read the
+# caller's Q/K/V (qmha_prepass.hip) keep default IEEE semantics (round-2 ADVICE)
 FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize", "-fno-honor-nans"] + os.environ.get("QMHA_INT8_FLAGS", "").split(),
               "qmha_fa_f16.hip": ["-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split(),
               "qmha_fa_f32.hip": os.environ.get("QMHA_F32_FLAGS", "").split()}
