@@ -282,7 +282,9 @@ float oracle_quantize_block(const float *src, int rows, int cols, int ld, int8_t
         for (int c = 0; c < cols; ++c) {
             float scaled = src[(size_t)r * ld + c] * inv; /* :137 */
             float rr = rintf(scaled);                     /* __float2int_rn: RNE */
-            int q = (int)fmaxf(fminf(rr, 2147483520.0f), -2147483648.0f);
+            /* __float2int_rn (PTX cvt.rni.s32.f32) saturates to the int range and converts NaN to 0
+               (fmaxf / fminf would turn a NaN into the clamp bound) */
+            int q = rr != rr ? 0 : (int)fmaxf(fminf(rr, 2147483520.0f), -2147483648.0f);
             q = q < -128 ? -128 : (q > 127 ? 127 : q); /* :139 */
             dst[(size_t)r * ldd + c] = (int8_t)q;
         }

@@ -115,6 +115,28 @@ def test_int8_quantised_bytes_and_scales_bitexact(dev, oracle_mod, N, d_model, h
     assert np.array_equal(Vg.cpu().numpy(), ref_t)
 
 
+def test_int8_nan_inputs(dev, oracle_mod):
+    """NaN in the caller's Q / K / V (the pre-passes keep IEEE semantics, round-2 ADVICE): the
+    reference's quantiser drops a NaN from the group absmax (fmaxf) and __float2int_rn turns it into
+    0, so the int8 path's output stays finite and equals the oracle's; the quantisation op writes the
+    same bytes and scales bit for bit."""
+    from quantizedmha_amd import torch_ext
+    N, dm, h = 256, 128, 2
+    Q, K, V = rand_inputs(61, 1, N, dm)
+    for X, pos in ((Q, [(3, 7), (100, 64)]), (K, [(0, 0), (37, 127)]), (V, [(200, 5), (31, 70)])):
+        for r, c in pos:
+            X[r, c] = np.nan
+    Xg, scg = torch_ext.quantize_int8(torch.from_numpy(K).to(dev), dm, h, layout=0)
+    Ki_ref, sk_ref = oracle_mod.quantize_heads(K, dm, h)
+    assert np.array_equal(scg.cpu().numpy(), sk_ref) and np.isfinite(sk_ref).all()
+    assert np.array_equal(Xg.cpu().numpy(), Ki_ref)
+    assert Ki_ref[0, 0, 0, 0] == 0 and Ki_ref[0, 1, 37, 63] == 0  # the NaN elements
+    out = run("fa_tc_int8_b", Q, K, V, dm, h, dev)
+    ref = oracle_mod.fa_int8(Q, K, V, dm, h)
+    assert np.isfinite(ref).all()
+    assert_parity("fa_tc_int8_b", out, ref)
+
+
 @pytest.mark.parametrize("N,d_model,h,head", [(128, 128, 2, 1), (256, 64, 2, 0), (64, 128, 1, 0), (128, 512, 4, 3)])
 def test_int8_qk_int32_bitexact(dev, oracle_mod, N, d_model, h, head):
     from quantizedmha_amd import torch_ext
