@@ -1028,7 +1028,20 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
         // (KFOLD: -2 % against plain MAGIC on one box, profiles/r01/overlap_sweep.txt)
         return fa_int8_pipe_launch<D, 4, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
     }
-    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
+    if constexpr (D == 32) {
+#ifdef QMHA_ABLATION
+        // workgroup size at d = 32 (122 VGPRs: 4 waves/SIMD, so an 8-wave workgroup keeps full
+        // occupancy, unlike d = 64): each LDS-DMA stage shared by more waves
+        static const int abl32 = std::getenv("QMHA_INT8_ABL") ? std::atoi(std::getenv("QMHA_INT8_ABL")) : 0;
+        switch (abl32) {
+            case 32081: return fa_int8_pipe_launch<D, 8, kD32Flags | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 32061: return fa_int8_pipe_launch<D, 6, kD32Flags | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 32041: return fa_int8_pipe_launch<D, 4, kD32Flags | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            default: break;
+        }
+#endif
+        return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
+    }
     return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
 }
 
