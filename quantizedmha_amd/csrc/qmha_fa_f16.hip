@@ -300,6 +300,9 @@ static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float
     return hipGetLastError();
 }
 
+#ifndef QMHA_F16_WAVES
+#define QMHA_F16_WAVES 8  // A/B builds: -DQMHA_F16_WAVES=4
+#endif
 #ifndef QMHA_F16_FL
 #define QMHA_F16_FL (F16_LB4 | F16_VPRE | F16_UNROLL)  // V operands before the softmax: -1.7 % (profiles/r02/ab/f16_vpre)
 #endif
@@ -321,13 +324,21 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
             case 447: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE>(w, Qf, O, B, N, H, d_model, stream);
             case 448: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 429: return fa_f16_v2_launch<D, 4, 2, F16_VPRE>(w, Qf, O, B, N, H, d_model, stream);
+            // workgroup size at the default flags (113 VGPRs: 4 waves/SIMD either way): each LDS-DMA
+            // stage shared by 8 / 16 waves (1 / 0.5 pieces per wave and tile instead of 2)
+            case 480: return fa_f16_v2_launch<D, 8, 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
+            case 4160: return fa_f16_v2_launch<D, 16, 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
+            case 484: return fa_f16_v2_launch<D, 8, 4, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
     }
 #endif
     // default: v2 (LDS-DMA staging, per-tile softmax), 4 waves/SIMD budget (r01 A/B: 1.54 ms vs
-    // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64)
-    return fa_f16_v2_launch<D, 4, 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
+    // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64), 8-wave workgroups: each LDS-DMA
+    // stage is shared by 8 waves (one 1-KiB piece per wave and tile instead of two) at the same
+    // occupancy (r03m: main -2.1 % against 4-wave workgroups, 16 waves +0 %, profiles/r03/ab/f16_wg).
+    // d = 128 keeps 4-wave workgroups: its 199 VGPRs do not fit the 8-wave register budget (111 spills)
+    return fa_f16_v2_launch<D, (D <= 64 ? QMHA_F16_WAVES : 4), 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,

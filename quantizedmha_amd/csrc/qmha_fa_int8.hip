@@ -1021,6 +1021,10 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             case 9081: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
             case 9121: return fa_int8_pipe_launch<D, 12, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
             case 9021: return fa_int8_pipe_launch<D, 2, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            // 4 waves/SIMD budget (operands read at their MFMA): 4- and 8-wave workgroups, the latter
+            // sharing each LDS-DMA stage between 8 waves at the same occupancy
+            case 9141: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9181: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif

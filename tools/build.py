@@ -21,8 +21,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "quantizedmha_amd", "csrc")
-OBJ = os.path.join(ROOT, "build", "obj")
-LIB = os.path.join(ROOT, "quantizedmha_amd", "lib")
+# QMHA_ALT=<name>: an A/B build of libqmha.so alone (own object dir, output in
+# quantizedmha_amd/alt_lib/<name>/), leaving the production build untouched
+ALT = os.environ.get("QMHA_ALT", "")
+OBJ = os.path.join(ROOT, "build", "obj_" + ALT if ALT else "obj")
+LIB = os.path.join(ROOT, "quantizedmha_amd", "alt_lib", ALT) if ALT else os.path.join(ROOT, "quantizedmha_amd", "lib")
 BIN = os.path.join(ROOT, "quantizedmha_amd", "bin")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -116,14 +119,18 @@ def build(jobs=8, verbose=True):
     os.makedirs(BIN, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, KERNEL_SOURCES))
-        shim_objs = {name: ex.submit(compile_one, "qmha_solve_variant.cpp",
-                                     (f"-DQMHA_SOLVE_VARIANT={vid}", f"-DQMHA_SOLVE_NAME={name}"))
-                     for name, vid in VARIANTS.items()}
-        drv_objs = list(ex.map(compile_one, DRIVER_SOURCES))
+        shim_objs = {} if ALT else {name: ex.submit(compile_one, "qmha_solve_variant.cpp",
+                                                    (f"-DQMHA_SOLVE_VARIANT={vid}", f"-DQMHA_SOLVE_NAME={name}"))
+                                    for name, vid in VARIANTS.items()}
+        drv_objs = [] if ALT else list(ex.map(compile_one, DRIVER_SOURCES))
         shim_objs = {k: v.result() for k, v in shim_objs.items()}
     libqmha = os.path.join(LIB, "libqmha.so")
     if newer(libqmha, objs):
         run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", libqmha] + objs)
+    if ALT:
+        if verbose:
+            print("built (A/B):", libqmha)
+        return libqmha
     for name, o in shim_objs.items():
         out = os.path.join(LIB, f"libqmha_{name}.so")
         if newer(out, [o, libqmha]):
