@@ -110,7 +110,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
        FL_DUMP = 256, FL_PIN = 512,
        FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
-       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072 };
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -516,6 +516,10 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     (void)QKop;
     constexpr int kSlot64[6] = {1, 1, 1, 1, 1, 1};
     constexpr int kOps64[6] = {0, 2, 1, 1000, 3, 1001};  // PV00 PV10 PV01 QK0 PV11 QK1
+    // FL_ACC1 (d = 64): ONE 16-register P@V accumulator for both d-blocks: PV00 PV01, block 0 folded
+    // into O in chunk D, PV10 PV11, block 1 folded at the iteration's end (16 VGPRs fewer)
+    constexpr bool ACC1 = (FL & FL_ACC1) && D == 64;
+    constexpr int kOps64a[6] = {0, 1, 1000, 2, 1001, 3};  // PV00 PV01 QK0 PV10 QK1 PV11
     constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
     constexpr int kOps32[3] = {0, 1, 1000};  // PV00 PV01 QK0
     constexpr int kSlot128[6] = {2, 2, 2, 2, 2, 2};
@@ -530,7 +534,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                                  QMHA_D128_SCHED ? 1 : 1001, QMHA_D128_SCHED ? 1001 : 1, 3, 5,
                                  QMHA_D128_SCHED ? 1002 : 7, QMHA_D128_SCHED ? 7 : 1002, 1003};
     auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
-    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]); };
+    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? (ACC1 ? kOps64a[i] : kOps64[i]) : kOps128[i]); };
     static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
     static_assert(NOPS == (D == 32 ? 3 : (D == 64 ? 6 : 12)), "MFMA schedule table");
 
@@ -708,8 +712,9 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                                 if (ks == 0) a[m] = v16f{};
                                 asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
                             } else {
-                                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
-                                                                              ks == 0 ? v16f{} : a[m], 0, 0, 0);
+                                v16f& acc = ACC1 ? a[0] : a[m];
+                                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                             ks == 0 ? v16f{} : acc, 0, 0, 0);
                             }
                         }
                     }
@@ -781,6 +786,10 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
             }
         }
         if constexpr (PIN) pin_regs(p, 0, 8);
+        if constexpr (ACC1 && has_prev) {  // block 0 of the pending tile (PV00, PV01 issued after A, B)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[0][r] = fmaf(a[0][r], scale_prev, o[0][r]);
+        }
         QMHA_FENCE();
         mfmas(3);
         QMHA_FENCE();
@@ -826,9 +835,9 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
         if constexpr (has_prev) {
 #pragma unroll
-            for (int m = 0; m < MB; ++m)
+            for (int m = ACC1 ? 1 : 0; m < MB; ++m)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[ACC1 ? 0 : m][r], scale_prev, o[m][r]);
         }
         if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
         QMHA_FENCE();
@@ -838,38 +847,224 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         scale_prev = scale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
+    // ---- FL_TSHADOW (d = 64): the same work, re-spaced around the MFMAs by instruction class.  On
+    // gfx950 an executing MFMA blocks the SIMD's full-rate fp32 VALU (v_fma/v_add/v_mul: no overlap)
+    // but not its transcendental and quarter-rate ops (v_exp, v_rcp, v_perm, v_max3, DPP, permlane):
+    // ~25 cycles of those hide per 32-cycle MFMA at 1-4 waves/SIMD (tools/ubench/mfma_fill.hip ->
+    // profiles/r03/ubench_mfma_fill.txt).  So every MFMA is followed by a group of such ops (the
+    // tile head after QK1 / PV11, four exps after each P@V / Q@K^T MFMA, the perms) and only then
+    // by the full-rate work (scores, quantisation, row sum, O folds), each group in its own
+    // sched_barrier region so the compiler keeps the order.
+    // MFMAs: m0 PV00, m1 PV10, m2 PV01, m3 QK0, m4 QK1, m5 PV11.  The O fold of d-block 0 of tile
+    // t-1 runs in this iteration (after m2), that of d-block 1 in the next one (after its head;
+    // scale_pp keeps tile t-1's scale for it)
+    constexpr bool TSHADOW = (FL & FL_TSHADOW) && D == 64;
+    static_assert(!(FL & FL_TSHADOW) || (D == 64 && KFOLD && !JIT && !ACC1 && !EARLY && !RING4 && !(FL & FL_DMA_SPLIT) &&
+                                         !NOMFMA && !NOMFMA2 && !NOEXP && !PIN),
+                  "FL_TSHADOW: d = 64 MAGIC|KFOLD schedule (no ablation / JIT / ring variants)");
+    float scale_pp = 0.0f;  // tile t-2's O scale for its d-block-1 fold (a[1] starts at 0: a no-op fold)
+    if constexpr (TSHADOW) a[1] = v16f{};
+    auto iter_ts = [&](int t, auto HP, auto HN, auto PH) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        if (odd) {  // uniform
+            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            if (dma_st < nst) issue_at(dma_st, dma_slot);
+        }
+        if constexpr (DUMP) {
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sd[8 * (r >> 2) + 4 * half + (r & 3)] = s_cur[r] - 0x4B400000;
+            }
+        }
+        // MFMA operands are read from LDS one region ahead of their MFMA (short live ranges)
+        v8h vv[MB][2];
+        v4i kk[KS];
+        auto rd_v = [&](int m, int ks) {
+            if constexpr (has_prev) vv[m][ks] = vop(m, ks);
+        };
+        auto rd_k = [&](int ks) {
+            if constexpr (has_next) kk[ks] = kop(ks);
+        };
+        auto pv = [&](int m, int ks) {
+            if constexpr (has_prev)
+                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][ks], pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+        };
+        auto qkm = [&](int ks) {
+            if constexpr (has_next) qk(kk[ks], ks);
+        };
+        rd_v(0, 0);
+        rd_v(1, 0);
+        float x[16], p[16], q[16];
+        auto exps = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        };
+        auto quant = [&](int r0, int r1) {  // Pi = rint(p/sP) in the low bits (f16 subnormal Pi * 2^-24)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
+        };
+        auto perms = [&](int j0, int j1) {  // pair j = rows 2j, 2j+1
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j >= j0 && j < j1) {
+                    const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(q[2 * j + 1]),
+                                                                               __float_as_uint(q[2 * j]), 0x05040100u));
+                    pc[j >> 2][2 * (j & 3)] = h2[0];
+                    pc[j >> 2][2 * (j & 3) + 1] = h2[1];
+                }
+            // pin: IR-level sinking (which sched_barrier does not constrain) would otherwise move the
+            // packs to their use in the next iteration, away from this MFMA shadow
+            asm volatile("" : "+v"(pc[0]), "+v"(pc[1]));
+        };
+        QMHA_FENCE();
+        // ---- R0 (behind m4 / m5 of the previous iteration): the tile head (row max tree, permlanes,
+        // DPP P-tile max, exp, rcp: quarter-rate / transcendental), the rare re-anchor
+        head(s_cur, t);
+        const float c = h_c, m_new = h_m, kn = h_k;
+        if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+            const float f = __builtin_amdgcn_exp2f(anchor - m_new);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= f;
+            l_run *= f;
+            scale_prev *= f;
+            scale_pp *= f;
+            anchor = m_new;
+        }
+        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
+        QMHA_FENCE();
+        // full rate: d-block 1 of tile t-2 (PV11 issued last iteration), scores 0..7
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        QMHA_FENCE();
+        pv(0, 0);  // m0
+        QMHA_FENCE();
+        exps(0, 4);
+        QMHA_FENCE();
+        rd_v(0, 1);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        quant(0, 4);
+        float rs0 = (p[0] + p[1]) + (p[2] + p[3]);
+        asm volatile("" : "+v"(rs0));
+        QMHA_FENCE();
+        pv(1, 0);  // m1
+        QMHA_FENCE();
+        exps(4, 8);
+        perms(0, 2);
+        QMHA_FENCE();
+        rd_k(0);
+        quant(4, 8);
+        float rs1 = (p[4] + p[5]) + (p[6] + p[7]);
+        asm volatile("" : "+v"(rs1));
+        QMHA_FENCE();
+        pv(0, 1);  // m2
+        QMHA_FENCE();
+        exps(8, 12);
+        perms(2, 4);
+        QMHA_FENCE();
+        rd_k(1);
+        quant(8, 12);
+        float rs2 = (p[8] + p[9]) + (p[10] + p[11]);
+        asm volatile("" : "+v"(rs2));
+        QMHA_FENCE();
+        qkm(0);  // m3
+        QMHA_FENCE();
+        exps(12, 16);
+        perms(4, 6);
+        QMHA_FENCE();
+        // d-block 0 of tile t-1 (PV00 m0, PV01 m2)
+        if constexpr (has_prev) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[0][r] = fmaf(a[0][r], scale_prev, o[0][r]);
+        }
+        rd_v(1, 1);
+        quant(12, 16);
+        float rs3 = (p[12] + p[13]) + (p[14] + p[15]);
+        asm volatile("" : "+v"(rs3));
+        QMHA_FENCE();
+        qkm(1);  // m4
+        QMHA_FENCE();
+        perms(6, 8);
+        QMHA_FENCE();
+        l_run = fmaf((rs0 + rs1) + (rs2 + rs3), e * h_f, l_run);
+        m_run = m_new;
+        const float scale_t = h_sp * svb[t] * e;
+        QMHA_FENCE();
+        pv(1, 1);  // m5
+        QMHA_FENCE();
+        // rotate the pipeline
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        scale_pp = has_prev ? scale_prev : 0.0f;
+        scale_prev = scale_t;
+        if constexpr (has_next) s_cur = s_nxt;
+    };
+    auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
+        if constexpr (TSHADOW)
+            iter_ts(t, HP, HN, PH);
+        else
+            iter(t, HP, HN, PH);
+    };
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
     // G >= 2 (the launcher routes N < 64 elsewhere): first, interior, last tile
     using DYN = std::integral_constant<int, -1>;
-    iter(0, F0{}, T1{}, DYN{});
+    run_iter(0, F0{}, T1{}, DYN{});
     int t = 1;
     constexpr int PER = 2 * RING;  // ring period in tiles
     for (; t + PER <= G - 1; t += PER) {
-        iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
-        iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
-        iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
-        iter(t + 3, T1{}, T1{}, std::integral_constant<int, 3>{});
-        iter(t + 4, T1{}, T1{}, std::integral_constant<int, 4>{});
-        iter(t + 5, T1{}, T1{}, std::integral_constant<int, 5>{});
+        run_iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
+        run_iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
+        run_iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
+        run_iter(t + 3, T1{}, T1{}, std::integral_constant<int, 3>{});
+        run_iter(t + 4, T1{}, T1{}, std::integral_constant<int, 4>{});
+        run_iter(t + 5, T1{}, T1{}, std::integral_constant<int, 5>{});
         if constexpr (RING4) {
-            iter(t + 6, T1{}, T1{}, std::integral_constant<int, 6>{});
-            iter(t + 7, T1{}, T1{}, std::integral_constant<int, 7>{});
+            run_iter(t + 6, T1{}, T1{}, std::integral_constant<int, 6>{});
+            run_iter(t + 7, T1{}, T1{}, std::integral_constant<int, 7>{});
         }
     }
-    for (; t < G - 1; ++t) iter(t, T1{}, T1{}, DYN{});
-    iter(G - 1, T1{}, F0{}, DYN{});
+    for (; t < G - 1; ++t) run_iter(t, T1{}, T1{}, DYN{});
+    run_iter(G - 1, T1{}, F0{}, DYN{});
 #undef QMHA_FENCE
-    // drain: P@V of the last tile
+    // drain: P@V of the last tile (TSHADOW: first the pending d-block-1 fold of tile G-2)
     {
         const int t = G - 1;
+        if constexpr (TSHADOW) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+            for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
+        }
+        if constexpr (ACC1) {
 #pragma unroll
-            for (int m = 0; m < MB; ++m)
-                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+            for (int m = 0; m < MB; ++m) {
+                a[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, 0), pp[0], v16f{}, 0, 0, 0);
+                a[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, 1), pp[1], a[0], 0, 0, 0);
+                o[m] += a[0] * scale_prev;
+            }
+        } else {
 #pragma unroll
-        for (int m = 0; m < MB; ++m) o[m] += a[m] * scale_prev;
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] += a[m] * scale_prev;
+        }
     }
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
     // lane (col, half) holds O^T rows d = 32 m + 8 g4 + 4 half + jj of query col
@@ -1025,6 +1220,12 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
             // sharing each LDS-DMA stage between 8 waves at the same occupancy
             case 9141: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
             case 9181: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            // one P@V accumulator block (FL_ACC1): at the default budget, and at 4 waves/SIMD with 4- / 8-wave workgroups
+            case 9200: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ACC1>(w, Qf, O, B, N, H, d_model, stream);
+            case 9241: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ACC1 | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9281: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD | FL_ACC1 | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            // MFMA shadows filled with transcendental / quarter-rate work (FL_TSHADOW)
+            case 9300: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_TSHADOW>(w, Qf, O, B, N, H, d_model, stream);
             default: break;
         }
 #endif
