@@ -31,8 +31,12 @@ typedef enum {
     QMHA_FA_TC_V1A = 1,    /* mha_kernels/fa_tc_v1a.cu  : fp16 MFMA, fp32 accumulation   */
     QMHA_FA_TC_INT8_B = 2, /* mha_kernels/fa_tc_int8_b.cu: int8 MFMA, per-32-row scales  */
     QMHA_UNFUSED = 3,      /* mha_kernels/unfused.cu    : QK^T, softmax, PV (3 kernels)   */
-    QMHA_FA_MFMA = 4       /* fa.cu's fp32 contract on v_mfma_f32_32x32x2_f32 (no reference
+    QMHA_FA_MFMA = 4,      /* fa.cu's fp32 contract on v_mfma_f32_32x32x2_f32 (no reference
                               counterpart: the matrix-core sibling of the scalar `fa`)    */
+    QMHA_FA_TC_INT8_PT = 5 /* per-tensor int8 mode (no reference counterpart: BASELINE.json's
+                              "per-tensor Q/K/V quant", SURVEY 0.2's optional flag): one scale
+                              per head slice of Q/K/V, static P scale 1/127, O accumulated on
+                              the matrix core                                              */
 } qmha_variant_t;
 
 /* Status codes of the extended entry points. */
@@ -88,7 +92,8 @@ int qmha_solve_variant(const float *Q, const float *K, const float *V, float *O,
  * x_i8 = clamp(rint(x / scale), -128, 127) (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
  * X: [B, N, d_model] fp32 device.  Xi: [B][h][N][d] int8 device.  scales: [B][h][N/32].
  * layout 0 = row-major rows (Q, K operand); layout 1 = V^T MFMA operand order
- * ([B][h][N/32][d][32], kv slots permuted as documented in DESIGN.md).
+ * ([B][h][N/32][d][32], kv slots permuted as documented in DESIGN.md); layout 2 = row-major rows
+ * with ONE scale per head slice (the fa_tc_int8_pt per-tensor mode; scales: [B][h]).
  */
 int qmha_quantize_int8(const float *X, int B, int N, int d_model, int h, int8_t *Xi, float *scales, int layout,
                        void *stream);

@@ -39,7 +39,7 @@ def lib():
             build()
         L = ctypes.CDLL(path)
         i, f, sz, l = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_long
-        for name in ("oracle_cpu_attention", "oracle_fa_int8", "oracle_fa_fp16", "oracle_fa_fp32"):
+        for name in ("oracle_cpu_attention", "oracle_fa_int8", "oracle_fa_fp16", "oracle_fa_fp32", "oracle_fa_int8_pt"):
             fn = getattr(L, name)
             fn.argtypes = [_f32p, _f32p, _f32p, _f32p, i, i, i, i, i]
             fn.restype = None
@@ -49,6 +49,8 @@ def lib():
         L.oracle_verify_results.restype = l
         L.oracle_quantize_heads.argtypes = [_f32p, i, i, i, i, ctypes.POINTER(ctypes.c_int8), _f32p]
         L.oracle_quantize_heads.restype = None
+        L.oracle_quantize_heads_pt.argtypes = [_f32p, i, i, i, i, ctypes.POINTER(ctypes.c_int8), _f32p]
+        L.oracle_quantize_heads_pt.restype = None
         L.oracle_qk_int32.argtypes = [ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_int8), i, i,
                                       ctypes.POINTER(ctypes.c_int32)]
         L.oracle_qk_int32.restype = None
@@ -110,6 +112,12 @@ def fa_int8(Q, K, V, d_model, h, nthreads=0):
     return _run4(lib().oracle_fa_int8, Q, K, V, d_model, h, nthreads)
 
 
+def fa_int8_pt(Q, K, V, d_model, h, nthreads=0):
+    """Per-tensor int8 mode (fa_tc_int8_pt; not a reference kernel: BASELINE.json's "per-tensor
+    Q/K/V quant", SURVEY 0.2's optional flag): per-head-slice scales, static P scale 1/127."""
+    return _run4(lib().oracle_fa_int8_pt, Q, K, V, d_model, h, nthreads)
+
+
 def fa_fp16(Q, K, V, d_model, h, nthreads=0):
     """mha_kernels/fa_tc_v1a.cu."""
     return _run4(lib().oracle_fa_fp16, Q, K, V, d_model, h, nthreads)
@@ -121,7 +129,7 @@ def fa_fp32(Q, K, V, d_model, h, nthreads=0):
 
 
 ORACLE_BY_VARIANT = {"fa_tc_int8_b": fa_int8, "fa_tc_v1a": fa_fp16, "fa": fa_fp32, "unfused": cpu_attention,
-                     "fa_mfma": fa_fp32}
+                     "fa_mfma": fa_fp32, "fa_tc_int8_pt": fa_int8_pt}
 
 
 def cpu_reference_rope(Q, K, V, d_model, h):
@@ -161,6 +169,17 @@ def quantize_heads(X, d_model, h):
     Xi = np.zeros((B, h, N, d), dtype=np.int8)
     sc = np.zeros((B, h, N // 32), dtype=np.float32)
     lib().oracle_quantize_heads(_p(X), B, N, d_model, h, _p(Xi, ctypes.c_int8), _p(sc))
+    return Xi, sc
+
+
+def quantize_heads_pt(X, d_model, h):
+    """Per-head-slice int8 quantisation (fa_tc_int8_pt): (Xi[B][h][N][d] int8, scales[B][h] fp32)."""
+    X = _c(X)
+    B, N = _shape(X, d_model)
+    d = d_model // h
+    Xi = np.zeros((B, h, N, d), dtype=np.int8)
+    sc = np.zeros((B, h), dtype=np.float32)
+    lib().oracle_quantize_heads_pt(_p(X), B, N, d_model, h, _p(Xi, ctypes.c_int8), _p(sc))
     return Xi, sc
 
 

@@ -417,6 +417,117 @@ void oracle_fa_int8(const float *Q, const float *K, const float *V, float *out,
 }
 
 /* ------------------------------------------------------------------------- */
+/* INT8, per-tensor mode (fa_tc_int8_pt).  NOT a reference kernel: BASELINE.json's
+ * "per-tensor Q/K/V quant" wording, offered beside the reference's per-block contract
+ * ("a per-tensor mode may be offered as an extra flag").  Same quantiser
+ * (fa_tc_int8_b.cu:33-152) applied to each head's whole [N, d] slice -- the matrix the
+ * reference's launch<> extracts per head (include/launchers.h:42-52) -- and P quantised with
+ * the static scale 1/127 (p = exp(s - m) lies in [0, 1]), so the P@V products of every tile
+ * share one unit and O accumulates as the int32 sums, rescaled by alpha only:
+ *   s = (float)(Qi.Ki)[int32] * sQ * sK * (1/sqrt(d)),  online softmax as fa_tc_int8_b (m0 = 0),
+ *   Pi = rint(p * 127),  O = alpha * O + (float)(Pi.Vi)[int32],
+ *   out = l > 1e-20 ? (O * (sV / 127)) / l : 0.                                  */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    const float *X;
+    int B, N, d_model, h;
+    int8_t *Xi;
+    float *scales;
+} qt_ctx;
+
+static void quantize_tensor_item(long bh, void *vctx) {
+    qt_ctx *c = (qt_ctx *)vctx;
+    int dh = c->d_model / c->h;
+    int b = (int)(bh / c->h), head = (int)(bh % c->h);
+    const float *src = c->X + (size_t)b * c->N * c->d_model + head * dh;
+    c->scales[bh] = oracle_quantize_block(src, c->N, dh, c->d_model, c->Xi + (size_t)bh * c->N * dh, dh);
+}
+
+void oracle_quantize_heads_pt(const float *X, int B, int N, int d_model, int h, int8_t *Xi, float *scales) {
+    qt_ctx c = {X, B, N, d_model, h, Xi, scales};
+    parallel_for((long)B * h, 0, quantize_tensor_item, &c);
+}
+
+static void fa_int8_pt_item(long item, void *vctx) {
+    int8_ctx *c = (int8_ctx *)vctx;
+    int N = c->N, dh = c->d_model / c->h, G = N / GROUP;
+    long bh = item / G;
+    int g = (int)(item % G);
+    int b = (int)(bh / c->h), head = (int)(bh % c->h);
+    const float inv_sqrt_d = 1.0f / sqrtf((float)dh);
+    const int8_t *Qg = c->Qi + ((size_t)bh * N + (size_t)g * GROUP) * dh;
+    const float sQ = c->sQ[bh], sK = c->sK[bh], sV = c->sV[bh];
+
+    float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
+    float l[GROUP], m_prev[GROUP];
+    for (int r = 0; r < GROUP; ++r) {
+        l[r] = 0.0f;
+        m_prev[r] = 0.0f; /* m0 = 0, as fa_tc_int8_b.cu:402 */
+    }
+    float s[GROUP][GROUP];
+    for (int t = 0; t < G; ++t) {
+        const int8_t *Kt = c->Ki + ((size_t)bh * N + (size_t)t * GROUP) * dh;
+        const int8_t *Vt = c->Vi + ((size_t)bh * N + (size_t)t * GROUP) * dh;
+        for (int r = 0; r < GROUP; ++r)
+            for (int j = 0; j < GROUP; ++j) {
+                int32_t acc = 0;
+                for (int k = 0; k < dh; ++k) acc += (int32_t)Qg[r * dh + k] * (int32_t)Kt[j * dh + k];
+                float deq = (float)acc * sQ * sK;
+                s[r][j] = deq * inv_sqrt_d;
+            }
+        for (int r = 0; r < GROUP; ++r) {
+            float m_new = m_prev[r];
+            for (int j = 0; j < GROUP; ++j) m_new = fmaxf(m_new, s[r][j]);
+            float lane[GROUP];
+            for (int j = 0; j < GROUP; ++j) {
+                s[r][j] = expf(s[r][j] - m_new);
+                lane[j] = s[r][j];
+            }
+            float sum_new = xor_tree_sum32(lane);
+            float alpha = expf(m_prev[r] - m_new);
+            l[r] = fmaf(alpha, l[r], sum_new);
+            for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
+            m_prev[r] = m_new;
+            int Pi[GROUP];
+            for (int j = 0; j < GROUP; ++j) {
+                float rr = rintf(s[r][j] * 127.0f); /* static P scale 1/127; p in [0, 1] */
+                Pi[j] = rr != rr ? 0 : (int)fminf(rr, 127.0f);
+            }
+            for (int d = 0; d < dh; ++d) {
+                int32_t acc = 0;
+                for (int j = 0; j < GROUP; ++j) acc += Pi[j] * (int32_t)Vt[j * dh + d];
+                O[r * dh + d] += (float)acc;
+            }
+        }
+    }
+    const float sVq = sV / 127.0f;
+    float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * c->d_model + head * dh;
+    for (int r = 0; r < GROUP; ++r)
+        for (int d = 0; d < dh; ++d)
+            out[(size_t)r * c->d_model + d] = (l[r] > 1e-20f) ? (O[r * dh + d] * sVq) / l[r] : 0.0f;
+    free(O);
+}
+
+void oracle_fa_int8_pt(const float *Q, const float *K, const float *V, float *out,
+                       int B, int N, int d_model, int h, int nthreads) {
+    int dh = d_model / h;
+    size_t ne = (size_t)B * h * N * dh, nbh = (size_t)B * h;
+    int8_t *Qi = (int8_t *)malloc(ne), *Ki = (int8_t *)malloc(ne), *Vi = (int8_t *)malloc(ne);
+    float *sQ = (float *)malloc(nbh * 4), *sK = (float *)malloc(nbh * 4), *sV = (float *)malloc(nbh * 4);
+    oracle_quantize_heads_pt(Q, B, N, d_model, h, Qi, sQ);
+    oracle_quantize_heads_pt(K, B, N, d_model, h, Ki, sK);
+    oracle_quantize_heads_pt(V, B, N, d_model, h, Vi, sV);
+    int8_ctx c = {B, N, d_model, h, Qi, Ki, Vi, sQ, sK, sV, out};
+    parallel_for((long)nbh * (N / GROUP), nthreads, fa_int8_pt_item, &c);
+    free(Qi);
+    free(Ki);
+    free(Vi);
+    free(sQ);
+    free(sK);
+    free(sV);
+}
+
+/* ------------------------------------------------------------------------- */
 /* FP16: mha_kernels/fa_tc_v1a.cu                                             */
 /* ------------------------------------------------------------------------- */
 typedef struct {

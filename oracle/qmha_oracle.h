@@ -62,6 +62,16 @@ void oracle_qk_int32(const int8_t *Qi, const int8_t *Ki, int N, int d, int32_t *
 void oracle_fa_int8(const float *Q, const float *K, const float *V, float *out,
                     int B, int N, int d_model, int h, int nthreads);
 
+/* Per-tensor int8 mode (fa_tc_int8_pt, not a reference kernel; see qmha_oracle.c): each
+ * head's [N, d] slice quantised with one scale (the fp32_to_int8sram arithmetic over the
+ * whole slice); scales[B][h]. */
+void oracle_quantize_heads_pt(const float *X, int B, int N, int d_model, int h,
+                              int8_t *Xi, float *scales);
+/* fa_tc_int8_pt: per-head-slice int8 Q/K/V, static P scale 1/127, int32 products, fp32
+ * online softmax with m0 = 0, O = alpha*O + (Pi.Vi), out = O*(sV/127)/l. */
+void oracle_fa_int8_pt(const float *Q, const float *K, const float *V, float *out,
+                       int B, int N, int d_model, int h, int nthreads);
+
 /* mha_kernels/fa_tc_v1a.cu:101-413 -- fp16 (RNE) operands, fp32 accumulation,
  * P stored as half(p), m0 = 0, epilogue guard 1e-10. */
 void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,

@@ -12,7 +12,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 # QMHA_LIB_PATH: load another build of the same C-ABI (A/B kernel experiments); still no fallback
 LIB_PATH = os.environ.get("QMHA_LIB_PATH") or os.path.join(LIB_DIR, "libqmha.so")
 
-VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4}
+VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4, "fa_tc_int8_pt": 5}
 DEFAULT_KERNEL = "fa_tc_int8_b"
 QMHA_OK = 0
 

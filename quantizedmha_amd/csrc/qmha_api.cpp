@@ -58,7 +58,7 @@ int check_shape(const void* Q, const void* K, const void* V, const void* O, int 
         g_last_error = "head size d = d_model/h must be 32, 64 or 128";
         return QMHA_ERR_NOSYS;
     }
-    if (variant < QMHA_FA || variant > QMHA_FA_MFMA) {
+    if (variant < QMHA_FA || variant > QMHA_FA_TC_INT8_PT) {
         g_last_error = "unknown variant";
         return QMHA_ERR_INVALID;
     }
@@ -185,6 +185,7 @@ int get_workspace(size_t need, hipStream_t stream, void** out) {
 size_t workspace_bytes(int B, int N, int H, int D, int variant) {
     switch (variant) {
         case QMHA_FA_TC_INT8_B: return qmha::int8_workspace_bytes(B, N, H, D);
+        case QMHA_FA_TC_INT8_PT: return qmha::int8_pt_workspace_bytes(B, N, H, D);
         case QMHA_FA_TC_V1A: return qmha::f16_workspace_bytes(B, N, H, D);
         case QMHA_UNFUSED: return qmha::unfused_workspace_bytes(B, N, H, D);
         default: return 0;
@@ -277,6 +278,16 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             }
             QMHA_MARK(rec.main, stream, false);
         }
+    } else if (variant == QMHA_FA_TC_INT8_PT) {
+        // per-tensor mode: group absmax of Q, K, V + K/V quantisation with the head-slice scales
+        // (two pre-pass launches), then the main kernel (Q quantised in registers)
+        const qmha::Int8Workspace w = qmha::int8_pt_carve(ws, B, N, h, D);
+        QMHA_MARK(rec.pre, stream, true);
+        QMHA_HIP_TRY(qmha::launch_quant_int8_pt(Q, K, V, w, B, N, h, D, d_model, stream), "quant_int8_pt launch");
+        QMHA_MARK(rec.pre, stream, false);
+        QMHA_MARK(rec.main, stream, true);
+        QMHA_HIP_TRY(qmha::launch_fa_int8_pt_main(w, Q, O, B, N, h, D, d_model, stream), "fa_int8_pt launch");
+        QMHA_MARK(rec.main, stream, false);
     } else if (variant == QMHA_FA || variant == QMHA_FA_MFMA) {
         QMHA_MARK(rec.main, stream, true);
         QMHA_HIP_TRY(qmha::launch_fa_f32(Q, K, V, O, B, N, h, D, d_model, variant == QMHA_FA_MFMA, stream),
@@ -359,9 +370,21 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
     int D = 0;
     int st = check_shape(X, X, X, Xi, B, N, d_model, h, QMHA_FA_TC_INT8_B, &D);
     if (st != QMHA_OK) return st;
-    if (!scales || (layout != 0 && layout != 1)) {
+    if (!scales || layout < 0 || layout > 2) {
         g_last_error = "bad scales pointer or layout";
         return QMHA_ERR_INVALID;
+    }
+    if (layout == 2) {  // per-tensor (head-slice) scales: group absmax pass + quantisation pass
+        const size_t need = qmha::align_up((size_t)3 * B * h * (N / 32) * sizeof(float), 256);
+        void* ws = nullptr;
+        st = get_workspace(need, (hipStream_t)stream, &ws);
+        if (st != QMHA_OK) return st;
+        qmha::Int8Workspace w{};
+        w.Ki = Xi;  // the K role: int8 rows
+        w.sK = scales;
+        w.gmax = static_cast<float*>(ws);
+        QMHA_HIP_TRY(qmha::launch_quant_int8_pt_rows(X, w, B, N, h, D, d_model, (hipStream_t)stream), "quant_int8_pt launch");
+        return QMHA_OK;
     }
     // The pre-pass kernel with X in one role only: the Q role (row layout) or the V role (the
     // V^T operand order); nothing else is written, no workspace is needed.
@@ -430,6 +453,7 @@ int qmha_variant_from_name(const char* name) {
     if (!std::strcmp(name, "fa_tc_int8_b")) return QMHA_FA_TC_INT8_B;
     if (!std::strcmp(name, "unfused")) return QMHA_UNFUSED;
     if (!std::strcmp(name, "fa_mfma")) return QMHA_FA_MFMA;
+    if (!std::strcmp(name, "fa_tc_int8_pt")) return QMHA_FA_TC_INT8_PT;
     return -1;
 }
 
@@ -440,6 +464,7 @@ const char* qmha_variant_name(int v) {
         case QMHA_FA_TC_INT8_B: return "fa_tc_int8_b";
         case QMHA_UNFUSED: return "unfused";
         case QMHA_FA_MFMA: return "fa_mfma";
+        case QMHA_FA_TC_INT8_PT: return "fa_tc_int8_pt";
         default: return "unknown";
     }
 }

@@ -51,8 +51,10 @@ __device__ __forceinline__ int chunk_swz(int row) {
 // the Q^T MFMA operand: lane (col, half) loads the D/2 values of query row `col` it feeds to
 // the i8 MFMA (bytes [32 s + 16 half, +16) of every k-step s), the wave reduces the group's
 // absmax.  Returns the group scale sQ.  Saves the pre-pass a third of its HBM traffic.
+// slice_sc > 0: the per-tensor mode's head-slice scale (no group absmax)
 template <int D>
-__device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, int half, v4i (&qop)[D / 32]) {
+__device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, int half, v4i (&qop)[D / 32],
+                                                 float slice_sc = 0.0f) {
     constexpr int KS = D / 32;
     v4f x[KS][4];
     float amax = 0.0f;
@@ -64,8 +66,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 #pragma unroll
             for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(x[s][c4][e]));
         }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);
+    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));
     const float inv = 1.0f / sc;
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -110,7 +111,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
        FL_DUMP = 256, FL_PIN = 512,
        FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
-       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288 };
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288, FL_PT = 1048576 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -397,7 +398,8 @@ template <int D, int WAVES, int FL, int PAD = 0>
 __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
+    const float* __restrict__ sQt = nullptr) {
     // FL_RING4 (d = 64): a 4-slot ring filled three stages ahead; the stage barrier waits with a
     // counted vmcnt (the newest stage's pieces stay in flight across it) instead of vmcnt(0)
     constexpr bool RING4 = FL & FL_RING4;
@@ -424,9 +426,15 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     v4i qop[D / 32];
     float cq = 0.0f;
     constexpr bool DUMP = FL & FL_DUMP;
+    // FL_PT (fa_tc_int8_pt, per-tensor mode): sQt / sK / sV hold one scale per head slice, P is
+    // quantised with the static scale 1/127, so every tile's P@V is in the same unit and
+    // accumulates straight into O (the MFMA C operand); O is rescaled by alpha when a row's
+    // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
+    constexpr bool PT = FL & FL_PT;
+    static_assert(!PT || !(FL & (FL_DUMP | FL_TSHADOW | FL_ACC1 | FL_ABL_NOMFMA | FL_ABL_NOMFMA2)), "FL_PT combinations");
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
-        const float sq = quant_q_operand<D>(qrow, half, qop);
+        const float sq = quant_q_operand<D>(qrow, half, qop, PT ? sQt[bh] : 0.0f);
         cq = sq * c_log2;
         if constexpr (DUMP) {  // the Q operand as held in registers: lane (col, half), k-step s
             int8_t* qd = dbg.Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
@@ -440,8 +448,8 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     }
     const int8_t* kbase = Ki + (size_t)bh * N * D;
     const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
-    const float* skb = sK + (size_t)bh * G;
-    const float* svb = sV + (size_t)bh * G;
+    const float* skb = sK + (size_t)bh * (PT ? 1 : G);  // PT: one scale per head slice
+    const float* svb = sV + (size_t)bh * (PT ? 1 : G);
     const int nst = (G + SG - 1) / SG;
 
     // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
@@ -588,13 +596,15 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // FL_EARLY: the serial head of a tile (row max -> running max -> P-tile max -> sP -> 1/sP)
     // runs at the end of the previous iteration, in one scheduling region with that
     // iteration's O update, so its latency chain interleaves with independent work
-    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f;
+    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f;
+    // PT: the score scale sQ * sK * log2(e) / sqrt(d) is one constant per head (KFOLD-rounded once)
+    const float c_pt = PT ? (KFOLD ? __int_as_float((__float_as_int(cq * skb[0]) + 2) & ~3) : cq * skb[0]) : 0.0f;
     auto head = [&](const v16i& s, int t) {
-        float c = cq * skb[t];
+        float c = PT ? c_pt : cq * skb[t];
         const int mxi = half_swap_max_i(tree_max16_i(s));
         float xmax;
         if constexpr (KFOLD) {
-            c = __int_as_float((__float_as_int(c) + 2) & ~3);
+            if constexpr (!PT) c = __int_as_float((__float_as_int(c) + 2) & ~3);
             const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;  // exact float(S_max)
             h_m = fmaxf(m_run, sfmax * c);
             h_k = fmaf(c, QMHA_MAGIC_RNE, h_m);
@@ -607,6 +617,12 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
             xmax = fmaf(mx, c, -h_m);
         }
         h_c = c;
+        if constexpr (PT) {  // alpha = 2^(m - m_new); Pi = rint(p * 127) (static P scale), f folded in
+            (void)xmax;
+            h_alpha = __builtin_amdgcn_exp2f(m_run - h_m);
+            h_invp = KFOLD ? 127.0f * h_f : 127.0f;
+            return;
+        }
         const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
         // sP = max(pmax / 127, 1e-8) as pm / 127 with pm = max(pmax, 127e-8), and 1/sP by one
         // v_rcp: within ~2 ulp of the reference's rounded 1/sP, which moves a Pi only when p/sP
@@ -712,9 +728,14 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                                 if (ks == 0) a[m] = v16f{};
                                 asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
                             } else {
-                                v16f& acc = ACC1 ? a[0] : a[m];
-                                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
-                                                                             ks == 0 ? v16f{} : acc, 0, 0, 0);
+                                if constexpr (PT) {  // P@V straight into O
+                                    o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                                  o[m], 0, 0, 0);
+                                } else {
+                                    v16f& acc = ACC1 ? a[0] : a[m];
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                                 ks == 0 ? v16f{} : acc, 0, 0, 0);
+                                }
                             }
                         }
                     }
@@ -730,7 +751,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
         // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
         // overflow it); the pending tile t-1 carries its factor in scale_prev
-        if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+        if (!PT && __builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
             const float f = __builtin_amdgcn_exp2f(anchor - m_new);
 #pragma unroll
             for (int m = 0; m < MB; ++m) o[m] *= f;
@@ -743,7 +764,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
-        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
+        const float e = PT ? 1.0f : __builtin_amdgcn_exp2f(m_new - anchor);
         float x[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -829,11 +850,20 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
         const float rs = tree_sum16(p);
-        l_run = fmaf(rs, KFOLD ? e * h_f : e, l_run);
+        if constexpr (PT)
+            l_run = fmaf(h_alpha, l_run, KFOLD ? rs * h_f : rs);  // l = alpha * l + sum(p)
+        else
+            l_run = fmaf(rs, KFOLD ? e * h_f : e, l_run);
         m_run = m_new;
-        const float scale_t = sp * svb[t] * e;  // sp carries 2^24: P entries are Pi * 2^-24
-        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
-        if constexpr (has_prev) {
+        const float scale_t = PT ? 0.0f : sp * svb[t] * e;  // sp carries 2^24: P entries are Pi * 2^-24
+        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor)); PT: O already
+        // holds tile t-1's P@V, and takes this tile's alpha before tile t's P@V lands next iteration
+        if constexpr (PT) {
+            if (__builtin_amdgcn_ballot_w64(h_alpha != 1.0f)) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m) o[m] *= h_alpha;
+            }
+        } else if constexpr (has_prev) {
 #pragma unroll
             for (int m = ACC1 ? 1 : 0; m < MB; ++m)
 #pragma unroll
@@ -1014,16 +1044,152 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         scale_prev = scale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
+    // ---- FL_PT at d = 64: the per-tensor iteration as explicit sched_barrier regions (the generic
+    // body above keeps its live ranges for the per-block fold and spills in this mode).  Every MFMA
+    // is followed by transcendental / quarter-rate work, full-rate work after it; operands are read
+    // one region ahead.  P@V accumulates straight into O; O takes tile t-1's alpha at the start of
+    // iteration t (before P@V of t-1 lands, after P@V of t-2 has), so no MFMA result is waited on.
+    // MFMAs: m0 PV00, m1 PV10, m2 PV01, m3 QK0, m4 QK1, m5 PV11.
+    float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
+    auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        if (odd) {  // uniform
+            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            if (dma_st < nst) issue_at(dma_st, dma_slot);
+        }
+        v8h vv[MB][2];
+        v4i kk[KS];
+        auto rd_v = [&](int m, int ks) {
+            if constexpr (has_prev) vv[m][ks] = vop_at(slot_p, par_p, m, ks);
+        };
+        auto rd_k = [&](int ks) {
+            if constexpr (has_next) kk[ks] = kop_at(slot_nx, par_n, ks);
+        };
+        auto pv = [&](int m, int ks) {
+            if constexpr (has_prev) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][ks], pp[ks], o[m], 0, 0, 0);
+        };
+        auto qkm = [&](int ks) {
+            if constexpr (has_next) qk(kk[ks], ks);
+        };
+        float x[16], p[16], q[16];
+        auto exps = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        };
+        auto quant = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
+        };
+        auto perms = [&](int j0, int j1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j >= j0 && j < j1) {
+                    const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(q[2 * j + 1]),
+                                                                               __float_as_uint(q[2 * j]), 0x05040100u));
+                    pc[j >> 2][2 * (j & 3)] = h2[0];
+                    pc[j >> 2][2 * (j & 3) + 1] = h2[1];
+                }
+            asm volatile("" : "+v"(pc[0]), "+v"(pc[1]));  // no IR-level sinking past this region
+        };
+        rd_v(0, 0);
+        rd_v(1, 0);
+        QMHA_FENCE();
+        // ---- R0: the tile head (quarter-rate / transcendental), then O *= alpha of tile t-1
+        head(s_cur, t);
+        const float c = h_c, kn = h_k;
+        QMHA_FENCE();
+        if constexpr (has_prev) {
+            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        pin_regs(x, 0, 8);
+        QMHA_FENCE();
+        pv(0, 0);  // m0
+        QMHA_FENCE();
+        exps(0, 4);
+        QMHA_FENCE();
+        rd_v(0, 1);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        pin_regs(x, 8, 16);
+        quant(0, 4);
+        float rs0 = (p[0] + p[1]) + (p[2] + p[3]);
+        asm volatile("" : "+v"(rs0));
+        QMHA_FENCE();
+        pv(1, 0);  // m1
+        QMHA_FENCE();
+        exps(4, 8);
+        perms(0, 2);
+        QMHA_FENCE();
+        rd_k(0);
+        quant(4, 8);
+        float rs1 = (p[4] + p[5]) + (p[6] + p[7]);
+        asm volatile("" : "+v"(rs1));
+        QMHA_FENCE();
+        pv(0, 1);  // m2
+        QMHA_FENCE();
+        exps(8, 12);
+        perms(2, 4);
+        QMHA_FENCE();
+        rd_k(1);
+        quant(8, 12);
+        float rs2 = (p[8] + p[9]) + (p[10] + p[11]);
+        asm volatile("" : "+v"(rs2));
+        QMHA_FENCE();
+        qkm(0);  // m3
+        QMHA_FENCE();
+        exps(12, 16);
+        perms(4, 6);
+        QMHA_FENCE();
+        rd_v(1, 1);
+        quant(12, 16);
+        float rs3 = (p[12] + p[13]) + (p[14] + p[15]);
+        asm volatile("" : "+v"(rs3));
+        QMHA_FENCE();
+        qkm(1);  // m4
+        QMHA_FENCE();
+        perms(6, 8);
+        QMHA_FENCE();
+        l_run = fmaf(h_alpha, l_run, ((rs0 + rs1) + (rs2 + rs3)) * h_f);  // l = alpha l + sum(p)
+        m_run = h_m;
+        QMHA_FENCE();
+        pv(1, 1);  // m5
+        QMHA_FENCE();
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        alpha_prev = h_alpha;
+        if constexpr (has_next) s_cur = s_nxt;
+    };
     auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
         if constexpr (TSHADOW)
             iter_ts(t, HP, HN, PH);
+        else if constexpr (PT && D == 64)
+            iter_pt(t, HP, HN, PH);
         else
             iter(t, HP, HN, PH);
     };
     using T1 = std::integral_constant<bool, true>;
     using F0 = std::integral_constant<bool, false>;
-    // G >= 2 (the launcher routes N < 64 elsewhere): first, interior, last tile
+    // G >= 2 (the per-block launcher routes N < 64 elsewhere): first, interior, last tile; G == 1
+    // (the per-tensor mode at N = 32): one tile, its P@V in the drain
     using DYN = std::integral_constant<int, -1>;
+    if (PT && G == 1) {
+        if constexpr (PT) run_iter(0, F0{}, F0{}, DYN{});
+    } else {
     run_iter(0, F0{}, T1{}, DYN{});
     int t = 1;
     constexpr int PER = 2 * RING;  // ring period in tiles
@@ -1041,6 +1207,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     }
     for (; t < G - 1; ++t) run_iter(t, T1{}, T1{}, DYN{});
     run_iter(G - 1, T1{}, F0{}, DYN{});
+    }
 #undef QMHA_FENCE
     // drain: P@V of the last tile (TSHADOW: first the pending d-block-1 fold of tile G-2)
     {
@@ -1049,7 +1216,19 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
         }
-        if constexpr (ACC1) {
+        if constexpr (PT) {
+            if constexpr (D == 64) {  // iter_pt: O still owes the last tile's alpha
+                if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+#pragma unroll
+                    for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
+                }
+            }
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
+        } else if constexpr (ACC1) {
 #pragma unroll
             for (int m = 0; m < MB; ++m) {
                 a[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, 0), pp[0], v16f{}, 0, 0, 0);
@@ -1069,8 +1248,10 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
     // lane (col, half) holds O^T rows d = 32 m + 8 g4 + 4 half + jj of query col
     if (active) {
-        const float unanchor = __builtin_amdgcn_exp2f(anchor - m_run);
-        const float l = half_swap_add(l_run) * unanchor;
+        // PT: O is in units of 2^-24 (the f16-subnormal P entries) times sV / 127: 2^24 * sV / 127
+        // rescales it exactly to the oracle's O * (sV / 127)
+        const float unanchor = PT ? 16777216.0f * (svb[0] / 127.0f) : __builtin_amdgcn_exp2f(anchor - m_run);
+        const float l = PT ? half_swap_add(l_run) : half_swap_add(l_run) * unanchor;
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
@@ -1118,7 +1299,7 @@ size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q) {
 }
 
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
-    Int8Workspace w;
+    Int8Workspace w{};
     const size_t e = align_up((size_t)B * H * N * D, 256);
     const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
     char* p = static_cast<char*>(ws);
@@ -1158,6 +1339,41 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
 #endif
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
                        w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
+    return hipGetLastError();
+}
+
+// ---- per-tensor mode (fa_tc_int8_pt) -----------------------------------------------------
+size_t int8_pt_workspace_bytes(int B, int N, int H, int D) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t s = align_up((size_t)B * H * sizeof(float), 256);
+    return e + 2 * e + g + 3 * s;
+}
+
+Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t s = align_up((size_t)B * H * sizeof(float), 256);
+    char* p = static_cast<char*>(ws);
+    Int8Workspace w{};
+    w.Ki = reinterpret_cast<int8_t*>(p);
+    w.Vh = reinterpret_cast<_Float16*>(p + e);
+    w.gmax = reinterpret_cast<float*>(p + 3 * e);
+    w.sQ = reinterpret_cast<float*>(p + 3 * e + g);
+    w.sK = reinterpret_cast<float*>(p + 3 * e + g + s);
+    w.sV = reinterpret_cast<float*>(p + 3 * e + g + 2 * s);
+    return w;
+}
+
+template <int D, int FL>
+static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                                    hipStream_t stream) {
+    constexpr int WAVES = 4;
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)w.sQ);
     return hipGetLastError();
 }
 
@@ -1248,6 +1464,16 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
         return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
     }
     return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
+}
+
+hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return fa_int8_pt_launch<32, kD32Flags | FL_PIN>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_pt_launch<128, kD128Flags | FL_PIN>(w, Qf, O, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,

@@ -19,9 +19,10 @@ struct Int8Workspace {
     int8_t* Qi;  // [B*H][N][D]  (test hook only: nullptr in the production carve)
     int8_t* Ki;  // [B*H][N][D]
     _Float16* Vh;  // [B*H][N/32][D][32]  quantised V as f16 integers (f16 operand slot order)
-    float* sQ;   // [B*H][N/32]
+    float* sQ;   // [B*H][N/32]  (per-tensor mode: [B*H], one scale per head slice)
     float* sK;
     float* sV;
+    float* gmax;  // per-tensor mode only: [3][B*H][N/32] group absmax of Q, K, V
 };
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
@@ -31,6 +32,18 @@ Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = fal
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
                              int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream,
                              int first_tensor = 0, int num_tensors = -1);
+// ---- INT8 per-tensor mode (fa_tc_int8_pt) ----------------------------------------------
+// layout: Ki, Vh as fa_tc_int8_b, then gmax [3][B*H][N/32], then sQ, sK, sV [B*H] each
+size_t int8_pt_workspace_bytes(int B, int N, int H, int D);
+Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D);
+// two launches: group absmax of Q, K, V; K and V quantised with their head-slice scales
+hipError_t launch_quant_int8_pt(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                                int H, int D, int d_model, hipStream_t stream);
+// the standalone op's per-tensor layout: X in the K role only (absmax pass over X, then int8 rows)
+hipError_t launch_quant_int8_pt_rows(const float* X, const Int8Workspace& w, int B, int N, int H, int D, int d_model,
+                                     hipStream_t stream);
+hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, hipStream_t stream);
 // Qf: the caller's fp32 Q (the main kernel quantises each Q group into its MFMA operand)
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream);

@@ -33,10 +33,11 @@ namespace qmha {
 // K/V are read exactly once per call.
 // v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
 // v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
+// slice_sc > 0: per-tensor mode, quantise with that scale (no per-group scale stored)
 template <int D, int VMODE>
 __device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void* __restrict__ Vout,
                                               float* __restrict__ sV, char* vtr, int lane, int b, int k, int g,
-                                              int bh, int N, int G, int d_model) {
+                                              int bh, int N, int G, int d_model, float slice_sc = 0.0f) {
     constexpr int C4 = D / 4, NI = 32 / (64 / C4);
     const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
     v4f x[NI];
@@ -48,21 +49,29 @@ __device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void*
 #pragma unroll
         for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
     }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);
+    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));
     const float inv = 1.0f / sc;
     if constexpr (VMODE == 1)
         vt_group_store<D, true>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
     else
         vt8_group_store<D>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
-    if (lane == 0) sV[(size_t)bh * G + g] = sc;
+    if (lane == 0 && slice_sc == 0.0f) sV[(size_t)bh * G + g] = sc;
+}
+
+// Per-tensor mode (fa_tc_int8_pt): the scale of a head's whole [N, d] slice from the absmax of
+// its G 32-row groups (qmha_group_absmax_kernel): max is exact in any order, so this equals the
+// fp32_to_int8sram arithmetic over the whole slice (fa_tc_int8_b.cu:56-106)
+__device__ __forceinline__ float slice_scale(const float* __restrict__ gmax, int G, int lane) {
+    float m = 0.0f;
+    for (int i = lane; i < G; i += 64) m = fmaxf(m, gmax[i]);
+    return qmha_scale_from_absmax(wave_max64(m));
 }
 
 // One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
 template <int D>
 __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int8_t* __restrict__ Xi,
                                                 float* __restrict__ sX, int lane, int b, int k, int g, int bh, int N,
-                                                int G, int d_model) {
+                                                int G, int d_model, float slice_sc = 0.0f) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
     const int ri = lane / C4, ci = lane % C4;
     v4f v[NI];
@@ -74,9 +83,8 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
 #pragma unroll
         for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
     }
-    amax = wave_max64(amax);
-    const float sc = qmha_scale_from_absmax(amax);  // :104
-    const float inv = 1.0f / sc;                     // :106 (correctly rounded division)
+    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));  // :104
+    const float inv = 1.0f / sc;                                                            // :106 (correctly rounded)
     int8_t* dst = Xi + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -85,19 +93,22 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
         for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
         *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
     }
-    if (lane == 0) sX[(size_t)bh * G + g] = sc;
+    if (lane == 0 && slice_sc == 0.0f) sX[(size_t)bh * G + g] = sc;
 }
 
 // ---------------------------------------------------------------------------------------
 // Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
 // One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
 // ---------------------------------------------------------------------------------------
-template <int D, int VMODE>
+// PT (per-tensor mode): gmax = [3][B*H][G] group absmax of Q, K, V (qmha_group_absmax_kernel);
+// every group of a head slice is quantised with the slice's scale; the group-0 wave of each
+// slice writes that scale to s{Q,K,V}[bh]
+template <int D, int VMODE, bool PT = false>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int first_tensor) {
+    int N, int H, int d_model, int total_groups, int first_tensor, const float* __restrict__ gmax = nullptr) {
     __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
     const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
@@ -107,11 +118,50 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const int G = N / QMHA_GROUP;
     const int bh = item / G, g = item % G;
     const int b = bh / H, k = bh % H;
+    float slice_sc = 0.0f;
+    if constexpr (PT) {
+        slice_sc = slice_scale(gmax + ((size_t)tensor * total_groups + (size_t)bh * G), G, lane);
+        float* s_out = tensor == 0 ? sQ : (tensor == 1 ? sK : sV);
+        if (g == 0 && lane == 0 && s_out) s_out[bh] = slice_sc;
+        if (tensor == 1 && g == 0 && sQ) {  // Q is quantised by the main kernel: its slice scale from here
+            const float sq = slice_scale(gmax + (size_t)bh * G, G, lane);
+            if (lane == 0) sQ[bh] = sq;
+        }
+    }
     if (tensor == 2)
-        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
+        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model, slice_sc);
     else
         quant_row_group<D>(tensor == 0 ? Q : K, tensor == 0 ? Qi : Ki, tensor == 0 ? sQ : sK, lane, b, k, g, bh, N, G,
-                           d_model);
+                           d_model, slice_sc);
+}
+
+// Per-tensor mode, first pass: the absmax of every 32-row group of every head of Q, K and V
+// (blockIdx.y = tensor), one wave per group, gmax = [3][B*H][G].  Reads the three fp32 tensors once.
+template <int D>
+__global__ __launch_bounds__(256) void qmha_group_absmax_kernel(const float* __restrict__ Q, const float* __restrict__ K,
+                                                                const float* __restrict__ V, float* __restrict__ gmax,
+                                                                int N, int H, int d_model, int total_groups,
+                                                                int first_tensor = 0) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
+    const int tensor = blockIdx.y + first_tensor;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + wave;
+    if (item >= total_groups) return;  // wave-uniform
+    const int G = N / QMHA_GROUP;
+    const int bh = item / G, g = item % G;
+    const int b = bh / H, k = bh % H;
+    const int ri = lane / C4, ci = lane % C4;
+    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
+    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+    float amax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const v4f v = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[c]));
+    }
+    amax = wave_max64(amax);
+    if (lane == 0) gmax[(size_t)tensor * total_groups + item] = amax;
 }
 
 
@@ -179,6 +229,50 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
         hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1>), grid, dim3(256), 0, stream, Q, K, V, w.Qi, w.Ki, vout, w.sQ,
                            w.sK, w.sV, N, H, d_model, total, first_tensor);
     return hipGetLastError();
+}
+
+template <int D>
+static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                                  int H, int d_model, hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.gmax, N,
+                       H, d_model, total);
+    // K and V quantised with their slice scales (blockIdx.y = tensor - 1); Q by the main kernel
+    hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V,
+                       nullptr, w.Ki, (void*)w.Vh, w.sQ, w.sK, w.sV, N, H, d_model, total, 1, (const float*)w.gmax);
+    return hipGetLastError();
+}
+
+template <int D>
+static hipError_t quant_int8_pt_rows_d(const float* X, const Int8Workspace& w, int B, int N, int H, int d_model,
+                                       hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    // X in the K role (tensor 1) of a [3][B*H][G] gmax table: absmax, then int8 rows + slice scales
+    hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X, w.gmax, N,
+                       H, d_model, total, 1);
+    hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X,
+                       nullptr, w.Ki, nullptr, nullptr, w.sK, nullptr, N, H, d_model, total, 1, (const float*)w.gmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_quant_int8_pt_rows(const float* X, const Int8Workspace& w, int B, int N, int H, int D, int d_model,
+                                     hipStream_t stream) {
+    switch (D) {
+        case 32: return quant_int8_pt_rows_d<32>(X, w, B, N, H, d_model, stream);
+        case 64: return quant_int8_pt_rows_d<64>(X, w, B, N, H, d_model, stream);
+        case 128: return quant_int8_pt_rows_d<128>(X, w, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_quant_int8_pt(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                                int H, int D, int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return quant_int8_pt_d<32>(Q, K, V, w, B, N, H, d_model, stream);
+        case 64: return quant_int8_pt_d<64>(Q, K, V, w, B, N, H, d_model, stream);
+        case 128: return quant_int8_pt_d<128>(Q, K, V, w, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,

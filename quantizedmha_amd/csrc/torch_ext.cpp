@@ -42,7 +42,7 @@ static Tensor flash_solve(const Tensor& Q, const Tensor& K, const Tensor& V, int
     const int64_t N = batched ? Qc.size(1) : q_elems / d_model;
     int variant = qmha_variant_from_name(kernel.c_str());
     if (variant < 0) {
-        TORCH_WARN("Kernel selection supports fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma; '", kernel,
+        TORCH_WARN("Kernel selection supports fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma, fa_tc_int8_pt; '", kernel,
                    "' routing to default 'fa_tc_int8_b'");
         variant = QMHA_FA_TC_INT8_B;
     }

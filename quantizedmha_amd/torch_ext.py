@@ -71,17 +71,18 @@ def quantize_int8(X: torch.Tensor, d_model: int, num_heads: int, layout: int = 0
     """The INT8 pre-pass as an op: per-32-row-group symmetric int8 of every head.
 
     Returns (Xi [B, h, N, d] int8 (layout 0) or [B, h, N/32, d, 32] (layout 1, V operand
-    order), scales [B, h, N/32] fp32)."""
+    order), scales [B, h, N/32] fp32); layout 2: [B, h, N, d] rows with one scale per head slice
+    (the fa_tc_int8_pt per-tensor mode), scales [B, h]."""
     if not X.is_cuda or X.dtype != torch.float32:
         raise RuntimeError("X must be a float32 CUDA tensor")
     Xc = X.contiguous()
     B, N = _shape(Xc, d_model)
     d = d_model // num_heads
-    if layout == 0:
+    if layout in (0, 2):
         Xi = torch.empty((B, num_heads, N, d), dtype=torch.int8, device=X.device)
     else:
         Xi = torch.empty((B, num_heads, N // 32, d, 32), dtype=torch.int8, device=X.device)
-    sc = torch.empty((B, num_heads, N // 32), dtype=torch.float32, device=X.device)
+    sc = torch.empty((B, num_heads) if layout == 2 else (B, num_heads, N // 32), dtype=torch.float32, device=X.device)
     with torch.cuda.device(Xc.device):
         stream = torch.cuda.current_stream(Xc.device).cuda_stream
         st = _lib.load().qmha_quantize_int8(Xc.data_ptr(), B, N, d_model, num_heads, Xi.data_ptr(), sc.data_ptr(),

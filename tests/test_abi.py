@@ -13,7 +13,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "launchers.h")
 LIB_DIR = os.path.join(ROOT, "quantizedmha_amd", "lib")
-VARIANTS = ["fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma"]
+VARIANTS = ["fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt"]
 
 
 def declared_functions():
@@ -168,13 +168,16 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
         if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
             dumps.append((d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
             continue
+        if m and int(m.group(2)) & 1048576:  # FL_PT: the fa_tc_int8_pt variant's own instance
+            name += "[pt]"
         per.setdefault((name, d), set()).add(rest)
     assert dumps
     for d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
         assert per[("qmha_fa_int8_pipe_kernel", d)] == {twin}, (d, twin)
     assert per, syms[:2000]
     for (name, d), inst in per.items():
-        limit = 2 if name == "qmha_quant_int8_kernel" else 1  # the V layout is a template argument
+        # the V layout and the per-tensor mode are template arguments of the quantiser
+        limit = 3 if name == "qmha_quant_int8_kernel" else 1
         assert len(inst) <= limit, (name, d, sorted(inst))
     blob = open(path, "rb").read()
     for env in (b"QMHA_INT8_CFG", b"QMHA_F16_CFG", b"QMHA_F32_CFG", b"QMHA_OVERLAP_CHUNKS", b"QMHA_INT8_ABL"):

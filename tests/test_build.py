@@ -30,7 +30,7 @@ def test_graft_entry_build_from_clean_copy(tmp_path):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     lib = dst / "quantizedmha_amd" / "lib"
     for name in ("libqmha.so", "libqmha_fa.so", "libqmha_fa_tc_v1a.so", "libqmha_fa_tc_int8_b.so",
-                 "libqmha_unfused.so", "libqmha_fa_mfma.so"):
+                 "libqmha_unfused.so", "libqmha_fa_mfma.so", "libqmha_fa_tc_int8_pt.so"):
         assert (lib / name).is_file(), name
     assert (dst / "quantizedmha_amd" / "bin" / "qmha_profile").is_file()
     assert (dst / "oracle" / "liboracle.so").is_file()
