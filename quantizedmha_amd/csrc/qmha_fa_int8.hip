@@ -384,6 +384,17 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
+// fa_tc_int8_pt's MFMA placement: the j-th (j < 2) MFMA issued after VALU region s (s < 6) of an
+// iteration, -1 for none; op 2m + ks = P@V of d-block m, k-step ks (tile t-1), op 8 + ks = Q@K^T
+// k-step ks (tile t+1).  P@V(m, 1) trails P@V(m, 0) by >= 2 slots; Q@K^T sits mid-iteration so
+// the next tile's scores land before its head.
+__host__ __device__ constexpr int pt_slot_op(int D, int s, int j) {
+    constexpr int d32[6][2] = {{0, -1}, {-1, -1}, {1, -1}, {8, -1}, {-1, -1}, {-1, -1}};
+    constexpr int d64[6][2] = {{0, -1}, {2, -1}, {1, -1}, {8, -1}, {9, -1}, {3, -1}};
+    constexpr int d128[6][2] = {{0, 2}, {4, 6}, {1, 3}, {8, 9}, {10, 11}, {5, 7}};
+    return D == 32 ? d32[s][j] : D == 64 ? d64[s][j] : d128[s][j];
+}
+
 template <int N>
 __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
 #pragma unroll
@@ -1044,12 +1055,13 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         scale_prev = scale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
-    // ---- FL_PT at d = 64: the per-tensor iteration as explicit sched_barrier regions (the generic
-    // body above keeps its live ranges for the per-block fold and spills in this mode).  Every MFMA
-    // is followed by transcendental / quarter-rate work, full-rate work after it; operands are read
-    // one region ahead.  P@V accumulates straight into O; O takes tile t-1's alpha at the start of
-    // iteration t (before P@V of t-1 lands, after P@V of t-2 has), so no MFMA result is waited on.
-    // MFMAs: m0 PV00, m1 PV10, m2 PV01, m3 QK0, m4 QK1, m5 PV11.
+    // ---- FL_PT: the per-tensor iteration as explicit sched_barrier regions (the generic body above
+    // keeps its live ranges for the per-block fold and spills in this mode).  Six regions R0..R5 of
+    // VALU work; after region s the MFMAs of pt_slot_op(D, s, .) issue (transcendental /
+    // quarter-rate work first in each region, full-rate work after it); operands are read from LDS
+    // in the region before their slot's predecessor (two slots ahead).  P@V accumulates straight
+    // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
+    // P@V of t-2 has), so no MFMA result is waited on.
     float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
     auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
@@ -1067,17 +1079,34 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         }
         v8h vv[MB][2];
         v4i kk[KS];
-        auto rd_v = [&](int m, int ks) {
-            if constexpr (has_prev) vv[m][ks] = vop_at(slot_p, par_p, m, ks);
+        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int op = pt_slot_op(D, s, j);
+                if (op >= 0 && op < 8) {
+                    if constexpr (has_prev)
+                        if ((op >> 1) < MB) vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
+                } else if (op >= 8) {
+                    if constexpr (has_next)
+                        if (op - 8 < KS) kk[(op - 8) % KS] = kop_at(slot_nx, par_n, op - 8);
+                }
+            }
         };
-        auto rd_k = [&](int ks) {
-            if constexpr (has_next) kk[ks] = kop_at(slot_nx, par_n, ks);
-        };
-        auto pv = [&](int m, int ks) {
-            if constexpr (has_prev) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][ks], pp[ks], o[m], 0, 0, 0);
-        };
-        auto qkm = [&](int ks) {
-            if constexpr (has_next) qk(kk[ks], ks);
+        auto mf_slot = [&](int s) {  // slot s's MFMAs
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int op = pt_slot_op(D, s, j);
+                if (op >= 0 && op < 8) {
+                    if constexpr (has_prev)
+                        if ((op >> 1) < MB) {
+                            const int m = (op >> 1) % MB;
+                            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][op & 1], pp[op & 1], o[m], 0, 0, 0);
+                        }
+                } else if (op >= 8) {
+                    if constexpr (has_next)
+                        if (op - 8 < KS) qk(kk[(op - 8) % KS], op - 8);
+                }
+            }
         };
         float x[16], p[16], q[16];
         auto exps = [&](int r0, int r1) {
@@ -1101,8 +1130,8 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                 }
             asm volatile("" : "+v"(pc[0]), "+v"(pc[1]));  // no IR-level sinking past this region
         };
-        rd_v(0, 0);
-        rd_v(1, 0);
+        rd_slot(0);
+        rd_slot(1);
         QMHA_FENCE();
         // ---- R0: the tile head (quarter-rate / transcendental), then O *= alpha of tile t-1
         head(s_cur, t);
@@ -1118,11 +1147,12 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
         pin_regs(x, 0, 8);
         QMHA_FENCE();
-        pv(0, 0);  // m0
+        mf_slot(0);
         QMHA_FENCE();
+        // ---- R1
         exps(0, 4);
         QMHA_FENCE();
-        rd_v(0, 1);
+        rd_slot(2);
 #pragma unroll
         for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
         pin_regs(x, 8, 16);
@@ -1130,44 +1160,48 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
         float rs0 = (p[0] + p[1]) + (p[2] + p[3]);
         asm volatile("" : "+v"(rs0));
         QMHA_FENCE();
-        pv(1, 0);  // m1
+        mf_slot(1);
         QMHA_FENCE();
+        // ---- R2
         exps(4, 8);
         perms(0, 2);
         QMHA_FENCE();
-        rd_k(0);
+        rd_slot(3);
         quant(4, 8);
         float rs1 = (p[4] + p[5]) + (p[6] + p[7]);
         asm volatile("" : "+v"(rs1));
         QMHA_FENCE();
-        pv(0, 1);  // m2
+        mf_slot(2);
         QMHA_FENCE();
+        // ---- R3
         exps(8, 12);
         perms(2, 4);
         QMHA_FENCE();
-        rd_k(1);
+        rd_slot(4);
         quant(8, 12);
         float rs2 = (p[8] + p[9]) + (p[10] + p[11]);
         asm volatile("" : "+v"(rs2));
         QMHA_FENCE();
-        qkm(0);  // m3
+        mf_slot(3);
         QMHA_FENCE();
+        // ---- R4
         exps(12, 16);
         perms(4, 6);
         QMHA_FENCE();
-        rd_v(1, 1);
+        rd_slot(5);
         quant(12, 16);
         float rs3 = (p[12] + p[13]) + (p[14] + p[15]);
         asm volatile("" : "+v"(rs3));
         QMHA_FENCE();
-        qkm(1);  // m4
+        mf_slot(4);
         QMHA_FENCE();
+        // ---- R5
         perms(6, 8);
         QMHA_FENCE();
         l_run = fmaf(h_alpha, l_run, ((rs0 + rs1) + (rs2 + rs3)) * h_f);  // l = alpha l + sum(p)
         m_run = h_m;
         QMHA_FENCE();
-        pv(1, 1);  // m5
+        mf_slot(5);
         QMHA_FENCE();
         pp[0] = pc[0];
         pp[1] = pc[1];
@@ -1177,7 +1211,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
         if constexpr (TSHADOW)
             iter_ts(t, HP, HN, PH);
-        else if constexpr (PT && D == 64)
+        else if constexpr (PT)
             iter_pt(t, HP, HN, PH);
         else
             iter(t, HP, HN, PH);
@@ -1217,11 +1251,9 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
             for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
         }
         if constexpr (PT) {
-            if constexpr (D == 64) {  // iter_pt: O still owes the last tile's alpha
-                if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {  // O still owes the last tile's alpha
 #pragma unroll
-                    for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
-                }
+                for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
             }
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -1469,9 +1501,9 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, hipStream_t stream) {
     switch (D) {
-        case 32: return fa_int8_pt_launch<32, kD32Flags | FL_PIN>(w, Qf, O, B, N, H, d_model, stream);
+        case 32: return fa_int8_pt_launch<32, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
         case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
-        case 128: return fa_int8_pt_launch<128, kD128Flags | FL_PIN>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }
