@@ -520,7 +520,9 @@ def reference_config(variant, dev, rank, world):
     h=32, so d=32) -- the shape of its published per-head times (README.md:19: 7.70 ms per head
     for fa_tc_int8_b on an L4).  One sequence, all 32 heads in one call; per-head ms beside it."""
     B, H, N, d = 1, 32, 8192, 32
-    rv = run_variant(variant, B, H, N, d, 10, 3, dev, rank, world)
+    # 20 warm-up calls (3 before r03p): the clock ramps over a fresh burst's first ~20 calls
+    # (tools/ramp.py -> profiles/r02/clock_ramp.txt)
+    rv = run_variant(variant, B, H, N, d, 20, 20, dev, rank, world)
     pub = {"fa_tc_int8_b": 7.70}.get(variant)
     return {"config": f"B{B} H{H} N{N} d{d} (include/config.h)",
             "ms_per_call": round(rv["ms_per_step"], 4),

@@ -1397,10 +1397,9 @@ Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D) {
     return w;
 }
 
-template <int D, int FL>
+template <int D, int FL, int WAVES = 4>
 static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                                     hipStream_t stream) {
-    constexpr int WAVES = 4;
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
@@ -1421,6 +1420,13 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
 #define QMHA_D128_FL (FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2)
 #endif
 constexpr int kD64Flags = QMHA_D64_FL, kD32Flags = QMHA_D32_FL, kD128Flags = QMHA_D128_FL;
+// per-tensor mode at d = 32: a 4-wave register budget (128 VGPRs; 131 otherwise, i.e. 3 waves/SIMD)
+#ifndef QMHA_PT_D32_EXTRA
+#define QMHA_PT_D32_EXTRA FL_LB4
+#endif
+#ifndef QMHA_PT_D32_WAVES
+#define QMHA_PT_D32_WAVES 4
+#endif
 
 // Default geometry per head size (QMHA_INT8_CFG tuning alternatives: QMHA_ABLATION builds only).
 template <int D>
@@ -1501,7 +1507,7 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, hipStream_t stream) {
     switch (D) {
-        case 32: return fa_int8_pt_launch<32, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
+        case 32: return fa_int8_pt_launch<32, kD32Flags | QMHA_PT_D32_EXTRA, QMHA_PT_D32_WAVES>(w, Qf, O, B, N, H, d_model, stream);
         case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
         case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;

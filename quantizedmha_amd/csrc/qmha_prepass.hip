@@ -5,8 +5,6 @@
 //                           head, sc = max(absmax/127, 1e-8), x_i8 = clamp(rint(x * (1/sc))) --
 //                           K as int8 rows, V as f16-valued integers in the MFMA V^T operand order
 //   qmha_convert_f16_kernel fa_tc_v1a.cu:300-330: K as f16 rows, V in the f16 V^T operand order (RNE)
-#include <algorithm>
-
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
@@ -233,40 +231,19 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
     return hipGetLastError();
 }
 
-// Batch chunks of at most ~QMHA_PT_CHUNK_BYTES of fp32 K + V: each chunk's absmax pass is followed
-// at once by its quantisation pass, whose re-read of K / V then comes from the 256 MiB Infinity
-// Cache instead of HBM (MI355X_MICROARCH.md: a table stays resident while it and the traffic between
-// its two uses fit in ~256 MiB)
-#ifndef QMHA_PT_CHUNK_BYTES
-#define QMHA_PT_CHUNK_BYTES (96u << 20)
-#endif
+// Two launches over the whole batch: the group absmax of Q, K, V, then K / V quantised with their
+// slice scales.  (r03: batch chunks of ~96 MiB of K + V, each absmax pass followed at once by its
+// quantisation so the re-read of K / V could come from the Infinity Cache, measured 0.260 against
+// 0.230 ms at C4, profiles/r03/pt/ab_chunk/)
 template <int D>
 static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                   int H, int d_model, hipStream_t stream) {
-    const int G = N / QMHA_GROUP;
-    const size_t seq_bytes = (size_t)2 * N * d_model * sizeof(float);  // K + V of one sequence
-    const int per = (int)std::max<size_t>(1, QMHA_PT_CHUNK_BYTES / seq_bytes);
-    for (int b0 = 0; b0 < B; b0 += per) {
-        const int nb = std::min(per, B - b0);
-        const size_t off = (size_t)b0 * N * d_model;  // floats
-        const size_t bh0 = (size_t)b0 * H;
-        const int total = nb * H * G;
-        // the chunk's views: tensors at the chunk's first sequence, gmax rows [tensor][bh0 + .][G]
-        // (the kernels index gmax by tensor * total_groups, so a chunk keeps its own packed table)
-        Int8Workspace c = w;
-        c.Ki = w.Ki + bh0 * N * D;
-        c.Vh = w.Vh + bh0 * N * D;
-        c.sQ = w.sQ + bh0;
-        c.sK = w.sK + bh0;
-        c.sV = w.sV + bh0;
-        c.gmax = w.gmax + (size_t)3 * bh0 * G;
-        hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q + off,
-                           K + off, V + off, c.gmax, N, H, d_model, total);
-        // K and V quantised with their slice scales (blockIdx.y = tensor - 1); Q by the main kernel
-        hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 2), dim3(256), 0, stream,
-                           Q + off, K + off, V + off, nullptr, c.Ki, (void*)c.Vh, c.sQ, c.sK, c.sV, N, H, d_model,
-                           total, 1, (const float*)c.gmax);
-    }
+    const int total = B * H * (N / QMHA_GROUP);
+    hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.gmax, N,
+                       H, d_model, total);
+    // K and V quantised with their slice scales (blockIdx.y = tensor - 1); Q by the main kernel
+    hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V,
+                       nullptr, w.Ki, (void*)w.Vh, w.sQ, w.sK, w.sV, N, H, d_model, total, 1, (const float*)w.gmax);
     return hipGetLastError();
 }
 
