@@ -17,7 +17,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 rc=$?; echo "rocprof trace rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/trace.log; exit $rc; }
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 find $OUT/trace -name "*kernel_trace.csv" -exec cp {} $OUT/kernel_trace.csv \;
-python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64" 30 50 > $OUT/trace_window.txt
+python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64ELi4ELi65E" 30 50 > $OUT/trace_window.txt
+python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64ELi4ELi1048641E" 2 25 >> $OUT/trace_window.txt
 python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_f16_v2_kernelILi64" 10 25 >> $OUT/trace_window.txt
 cat $OUT/trace_window.txt
 exit 0
