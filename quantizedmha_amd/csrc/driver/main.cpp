@@ -44,7 +44,7 @@ static void usage(const char* argv0) {
         "Usage: %s [--kernel=KERNEL] [--warmup=N] [--runs=M] [--check=0|1] [--no-check] [--random]\n"
         "          [--B=1] [--N=8192] [--d_model=1024] [--h=32] [--check-random] [--threads=T]\n"
         "          [--cache-dir=.cache] [--json]\n"
-        "  KERNEL options: fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma\n",
+        "  KERNEL options: fa, fa_tc_v1a, fa_tc_int8_b, unfused, fa_mfma, fa_tc_int8_pt\n",
         argv0);
 }
 
@@ -187,7 +187,8 @@ int main(int argc, char** argv) {
         std::printf("Computing CPU attention (no RoPE, %d threads) for the random-data check...\n", threads);
         cpu_attention(hQ, hK, hV, ref, N, d_model, h, threads);
         // tolerances: fp32 1e-5, fp16 1e-3 (verify.cu default), int8 5e-3 (quantisation error)
-        const float tol = variant == QMHA_FA_TC_INT8_B ? 5e-3f : (variant == QMHA_FA_TC_V1A ? 1e-3f : 1e-5f);
+        const bool int8 = variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_INT8_PT;
+        const float tol = int8 ? 5e-3f : (variant == QMHA_FA_TC_V1A ? 1e-3f : 1e-5f);
         const bool ok = verify_results(hO, ref, tol, tol, &max_err);
         rand_status = ok ? "passed" : "failed";
         std::printf("Random-data check %s (max abs err %.3g, tol %.1g).\n", rand_status, max_err, tol);
