@@ -12,6 +12,7 @@
  *   libqmha_fa.so              `solve` bound to the scalar path    (make KERNEL=fa)
  *   libqmha_fa_mfma.so         `solve` bound to fa's contract on the fp32 matrix cores
  *   libqmha_unfused.so         `solve` bound to the 3-kernel path  (make KERNEL=unfused)
+ *   libqmha_fa_tc_int8_pt.so   `solve` bound to the per-tensor int8 mode (no reference kernel)
  * mirroring the reference's one-kernel-per-binary build (Makefile:39-53,
  * extensions/torch/setup.py:21-43).
  */
@@ -116,7 +117,7 @@ int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int 
 int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                             int h, int32_t *S, int8_t *Qi, float *sQ);
 
-/* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma") -> id, or -1. */
+/* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);
 const char *qmha_variant_name(int variant);
 const char *qmha_status_string(int status);
