@@ -408,6 +408,12 @@ def main():
                    "parallelism": f"batch-shard x{world} (no collective in the timed step; all-gather reported "
                                   f"separately)"},
     }
+    if a.variant == "fa_tc_int8_b":
+        # BASELINE config 4 reads "per-tensor Q/K/V quant"; the reference kernel quantises per 32-row
+        # block, which is the headline; the per-tensor mode is its own variant, summarised
+        # below as int8_per_tensor
+        res["config"]["quantisation"] = ("per-32-row-block Q/K/V scales, per 32x32-tile P scale (the reference's "
+                                         "fa_tc_int8_b numerics)")
     if dry:
         res["dry_run"] = True
     else:
@@ -437,6 +443,14 @@ def main():
         }
     del r
     res.update(side)
+    pt = side.get("siblings", {}).get("fa_tc_int8_pt")
+    if pt and a.variant == "fa_tc_int8_b":
+        res["int8_per_tensor"] = {
+            "variant": "fa_tc_int8_pt", "config": pt["config"],
+            "quantisation": "one scale per (sequence, head) slice of Q/K/V, static P scale 1/127 (DESIGN.md 3.1)",
+            "value": pt["tflops"], "unit": "TFLOPS", "ms_per_step": pt["ms_per_step"],
+            "main_kernel_ms": pt["main_kernel_ms"], "prepass_ms": pt["prepass_ms"],
+            "roofline_frac": pt["roofline_frac"]}
     if not a.no_siblings and not dry and world == 1:
         res["torch_ext"] = time_torch_ext(B, H, N, d, dev)
     if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls and not dry:
