@@ -451,6 +451,10 @@ def main():
             "value": pt["tflops"], "unit": "TFLOPS", "ms_per_step": pt["ms_per_step"],
             "main_kernel_ms": pt["main_kernel_ms"], "prepass_ms": pt["prepass_ms"],
             "roofline_frac": pt["roofline_frac"]}
+        tr, tr_src = pmc_traffic("fa_tc_int8_pt", B, H, N, d)
+        busy_pt, busy_pt_src = pmc_sq("fa_tc_int8_pt", B, H, N, d)
+        res["int8_per_tensor"].update({"traffic": tr, "traffic_source": tr_src, "mfma_busy_pct": busy_pt,
+                                       "mfma_busy_source": busy_pt_src})
     if not a.no_siblings and not dry and world == 1:
         res["torch_ext"] = time_torch_ext(B, H, N, d, dev)
     if rank == 0 and world == 1 and not a.no_siblings and not a.no_solve_calls and not dry:
