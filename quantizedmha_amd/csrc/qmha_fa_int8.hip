@@ -111,7 +111,8 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
        FL_DUMP = 256, FL_PIN = 512,
        FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
-       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288, FL_PT = 1048576 };
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288, FL_PT = 1048576,
+       FL_FAIR = 2097152 };
 
 template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
 __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
@@ -402,6 +403,15 @@ __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
         if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
 }
 
+#ifdef QMHA_TIMELINE  // profiling builds only: per-workgroup start / end wall clock of the last launch
+__device__ unsigned long long qmha_tl_buf[4][1 << 17];
+__device__ __forceinline__ unsigned long long qmha_tl_now() { return wall_clock64(); }
+extern "C" int qmha_debug_timeline(unsigned long long* host) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(host, HIP_SYMBOL(qmha_tl_buf), sizeof(qmha_tl_buf));
+    return (int)e;
+}
+#endif
 #ifndef QMHA_PIPE_ATTR  // profiling builds may cap the register budget, e.g. amdgpu_num_vgpr
 #define QMHA_PIPE_ATTR
 #endif
@@ -424,6 +434,9 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     __shared__ __attribute__((aligned(16))) int8_t lds[RING][SBYTES];
 
     QMHA_ENABLE_AGPR_MFMA();
+#ifdef QMHA_TIMELINE
+    const unsigned long long tl_t0 = qmha_tl_now();
+#endif
     const int G = N / QMHA_GROUP;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = wg / nqb, qb = wg % nqb;
@@ -442,6 +455,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // accumulates straight into O (the MFMA C operand); O is rescaled by alpha when a row's
     // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
     constexpr bool PT = FL & FL_PT;
+    constexpr bool FAIR = FL & FL_FAIR;
     static_assert(!PT || !(FL & (FL_DUMP | FL_TSHADOW | FL_ACC1 | FL_ABL_NOMFMA | FL_ABL_NOMFMA2)), "FL_PT combinations");
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
@@ -1224,10 +1238,29 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     if (PT && G == 1) {
         if constexpr (PT) run_iter(0, F0{}, F0{}, DYN{});
     } else {
+    // FL_FAIR: a workgroup's waves lower their issue priority as their sweep progresses (3 in the
+    // first quarter of the tiles .. 0 in the last), so the co-resident workgroups of a SIMD -- which
+    // the age-ordered arbiter would otherwise finish one after another -- advance together and the
+    // kernel does not end on a few workgroups running alone (tools/timeline.py)
+    auto set_prio = [&](int tt) {
+        if constexpr (FAIR) {
+            const int q = (4 * tt) / G;  // wave-uniform
+            if (q <= 0)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+    };
+    set_prio(0);
     run_iter(0, F0{}, T1{}, DYN{});
     int t = 1;
     constexpr int PER = 2 * RING;  // ring period in tiles
     for (; t + PER <= G - 1; t += PER) {
+        set_prio(t);
         run_iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
         run_iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
         run_iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
@@ -1296,6 +1329,17 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
                 *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
             }
     }
+#ifdef QMHA_TIMELINE
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 17)) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        qmha_tl_buf[0][blockIdx.x] = tl_t0;
+        qmha_tl_buf[1][blockIdx.x] = qmha_tl_now();
+        qmha_tl_buf[2][blockIdx.x] = hw;
+        qmha_tl_buf[3][blockIdx.x] = xcc;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
