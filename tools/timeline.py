@@ -50,8 +50,13 @@ def main():
     print(f"{variant} B{B} H{H} N{N} d{d}: {nwg} workgroups, span {span:.1f} us (first start -> last end)")
     print(f"  workgroup duration: mean {dur.mean():.1f} us, min {dur.min():.1f}, p50 {np.median(dur):.1f}, "
           f"p95 {np.percentile(dur, 95):.1f}, max {dur.max():.1f}")
-    first = (s < 2.0).sum()
+    r1 = s < 2.0
+    first = r1.sum()
     print(f"  started within 2 us: {first} workgroups (the first round); last start at {s.max():.1f} us")
+    later = ~r1 & (s < s.max() - dur.mean())  # neither the first round nor the drain
+    print(f"  duration, first round: mean {dur[r1].mean():.1f} us (p05 {np.percentile(dur[r1], 5):.1f}, p95 "
+          f"{np.percentile(dur[r1], 95):.1f}); steady-state starts: "
+          + (f"mean {dur[later].mean():.1f} us (n={later.sum()})" if later.any() else "none"))
     grid = np.linspace(0, span, 201)
     resident = np.array([((s <= t) & (e > t)).sum() for t in grid])
     peak = resident.max()
