@@ -117,6 +117,12 @@ int qmha_debug_qk_int32(const float *Q, const float *K, int N, int d_model, int 
 int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                             int h, int32_t *S, int8_t *Qi, float *sQ);
 
+/* As qmha_debug_fa_int8_dump for the per-tensor mode (QMHA_FA_TC_INT8_PT): its production schedule
+ * plus the stores; Qi is quantised with the head slice's scale, and sQ[B*h][N/32] holds that one
+ * scale in every group's entry.  N >= 32.  Device pointers; blocking. */
+int qmha_debug_fa_int8_pt_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
+                               int h, int32_t *S, int8_t *Qi, float *sQ);
+
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);
 const char *qmha_variant_name(int variant);

@@ -27,6 +27,7 @@ SIGNATURES = {
     "qmha_quantize_int8": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp]),
     "qmha_debug_qk_int32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "qmha_debug_fa_int8_dump": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "qmha_debug_fa_int8_pt_dump": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     "qmha_variant_from_name": (_i, [_cp]),
     "qmha_variant_name": (_cp, [_i]),
     "qmha_status_string": (_cp, [_i]),

@@ -446,6 +446,27 @@ int qmha_debug_fa_int8_dump(const float* Q, const float* K, const float* V, floa
     return QMHA_OK;
 }
 
+int qmha_debug_fa_int8_pt_dump(const float* Q, const float* K, const float* V, float* O, int B, int N, int d_model,
+                               int h, int32_t* S, int8_t* Qi, float* sQ) {
+    int D = 0;
+    int st = check_shape(Q, K, V, O, B, N, d_model, h, QMHA_FA_TC_INT8_PT, &D);
+    if (st != QMHA_OK) return st;
+    if (!S || !Qi || !sQ) {
+        g_last_error = "debug dump: needs S/Qi/sQ buffers";
+        return QMHA_ERR_INVALID;
+    }
+    const size_t need = qmha::int8_pt_workspace_bytes(B, N, h, D);
+    void* ws = nullptr;
+    st = get_workspace(need, nullptr, &ws);
+    if (st != QMHA_OK) return st;
+    const qmha::Int8Workspace w = qmha::int8_pt_carve(ws, B, N, h, D);
+    QMHA_HIP_TRY(qmha::launch_quant_int8_pt(Q, K, V, w, B, N, h, D, d_model, nullptr), "quant_int8_pt launch");
+    QMHA_HIP_TRY(qmha::launch_fa_int8_pt_dump(w, Q, O, B, N, h, D, d_model, qmha::QkDump{S, Qi, sQ}, nullptr),
+                 "fa_int8_pt dump launch");
+    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    return QMHA_OK;
+}
+
 int qmha_variant_from_name(const char* name) {
     if (!name) return -1;
     if (!std::strcmp(name, "fa")) return QMHA_FA;

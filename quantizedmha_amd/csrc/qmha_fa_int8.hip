@@ -456,7 +456,7 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
     constexpr bool PT = FL & FL_PT;
     constexpr bool FAIR = FL & FL_FAIR;
-    static_assert(!PT || !(FL & (FL_DUMP | FL_TSHADOW | FL_ACC1 | FL_ABL_NOMFMA | FL_ABL_NOMFMA2)), "FL_PT combinations");
+    static_assert(!PT || !(FL & (FL_TSHADOW | FL_ACC1 | FL_ABL_NOMFMA | FL_ABL_NOMFMA2)), "FL_PT combinations");
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
         const float sq = quant_q_operand<D>(qrow, half, qop, PT ? sQt[bh] : 0.0f);
@@ -1091,6 +1091,13 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
             qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
             if (dma_st < nst) issue_at(dma_st, dma_slot);
         }
+        if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (32x32 accumulator map)
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sd[8 * (r >> 2) + 4 * half + (r & 3)] = s_cur[r] - 0x4B400000;
+            }
+        }
         v8h vv[MB][2];
         v4i kk[KS];
         auto rd_slot = [&](int s) {  // operands of slot s's MFMAs
@@ -1443,12 +1450,12 @@ Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D) {
 
 template <int D, int FL, int WAVES = 4>
 static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, QkDump dbg = QkDump{}) {
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
-                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)w.sQ);
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ);
     return hipGetLastError();
 }
 
@@ -1578,6 +1585,20 @@ hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O
         case 64: return fa_int8_pipe_launch<64, 4, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 128:
             return fa_int8_pipe_launch<128, 4, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The per-tensor mode's production schedule with FL_DUMP (same flags and workgroup size as
+// launch_fa_int8_pt_main, plus the stores)
+hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, QkDump dbg, hipStream_t stream) {
+    switch (D) {
+        case 32:
+            return fa_int8_pt_launch<32, kD32Flags | QMHA_PT_D32_EXTRA | FL_DUMP, QMHA_PT_D32_WAVES>(w, Qf, O, B, N, H,
+                                                                                                 d_model, stream, dbg);
+        case 64: return fa_int8_pt_launch<64, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 128: return fa_int8_pt_launch<128, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         default: return hipErrorInvalidValue;
     }
 }

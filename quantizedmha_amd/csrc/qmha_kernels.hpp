@@ -57,6 +57,8 @@ struct QkDump {
 };
 hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, QkDump dbg, hipStream_t stream);
+hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, QkDump dbg, hipStream_t stream);
 
 // ---- FP16 (fa_tc_v1a) ------------------------------------------------------------------
 struct F16Workspace {

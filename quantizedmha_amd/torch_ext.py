@@ -105,10 +105,12 @@ def debug_qk_int32(Q: torch.Tensor, K: torch.Tensor, d_model: int, num_heads: in
     return S
 
 
-def debug_fa_int8_dump(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int):
+def debug_fa_int8_dump(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_model: int, num_heads: int,
+                       per_tensor: bool = False):
     """Run the production int8 kernel with its FL_DUMP stores (test hook): returns (O, S, Qi, sQ)
     with O as flash_solve computes it, S [B, h, N, N] int32 = the kernel's own Q@K^T
-    accumulators (bias removed), Qi [B, h, N, d] its in-register int8 Q operand, sQ [B, h, N/32]."""
+    accumulators (bias removed), Qi [B, h, N, d] its in-register int8 Q operand, sQ [B, h, N/32].
+    per_tensor: the fa_tc_int8_pt kernel instead (sQ then repeats the head slice's one scale)."""
     if not (Q.is_cuda and K.is_cuda and V.is_cuda):
         raise RuntimeError("Inputs must be CUDA tensors")
     Qc, Kc, Vc = Q.contiguous(), K.contiguous(), V.contiguous()
@@ -120,7 +122,9 @@ def debug_fa_int8_dump(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_mode
     sQ = torch.empty((B, num_heads, N // 32), dtype=torch.float32, device=Q.device)
     torch.cuda.synchronize(Q.device)
     with torch.cuda.device(Qc.device):
-        st = _lib.load().qmha_debug_fa_int8_dump(Qc.data_ptr(), Kc.data_ptr(), Vc.data_ptr(), O.data_ptr(), B, N,
-                                                 d_model, num_heads, S.data_ptr(), Qi.data_ptr(), sQ.data_ptr())
+        lib = _lib.load()
+        fn = lib.qmha_debug_fa_int8_pt_dump if per_tensor else lib.qmha_debug_fa_int8_dump
+        st = fn(Qc.data_ptr(), Kc.data_ptr(), Vc.data_ptr(), O.data_ptr(), B, N, d_model, num_heads, S.data_ptr(),
+                Qi.data_ptr(), sQ.data_ptr())
     _lib.check(st, "debug_fa_int8_dump")
     return O, S, Qi, sQ

@@ -165,15 +165,15 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
         if name.startswith("qmha_gemm"):
             continue
         m = re.match(r"Li(\d+)ELi(\d+)E", rest) if name == "qmha_fa_int8_pipe_kernel" else None
-        if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
-            dumps.append((d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
-            continue
         if m and int(m.group(2)) & 1048576:  # FL_PT: the fa_tc_int8_pt variant's own instance
             name += "[pt]"
+        if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
+            dumps.append((name, d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
+            continue
         per.setdefault((name, d), set()).add(rest)
-    assert dumps
-    for d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
-        assert per[("qmha_fa_int8_pipe_kernel", d)] == {twin}, (d, twin)
+    assert len(dumps) == 6, dumps  # per-block and per-tensor, d = 32 / 64 / 128
+    for name, d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
+        assert per[(name, d)] == {twin}, (name, d, twin)
     assert per, syms[:2000]
     for (name, d), inst in per.items():
         # the V layout and the per-tensor mode are template arguments of the quantiser

@@ -221,6 +221,35 @@ def test_production_qk_int32_bitexact(dev, oracle_mod, B, N, h, d, heads):
         assert np.array_equal(S[b, k].cpu().numpy(), S_ref), (b, k)
 
 
+@pytest.mark.parametrize("B,N,h,d,heads", [(1, 32, 2, 64, None), (2, 96, 1, 64, None), (1, 4096, 2, 64, None),
+                                            (2, 4096, 16, 64, [(0, 3), (1, 12)]), (1, 160, 2, 32, None),
+                                            (1, 8192, 32, 32, [(0, 0), (0, 31)]), (2, 128, 2, 128, None),
+                                            (1, 2048, 4, 128, [(0, 2)])])
+def test_production_qk_int32_bitexact_per_tensor(dev, oracle_mod, B, N, h, d, heads):
+    """As test_production_qk_int32_bitexact for the per-tensor mode (fa_tc_int8_pt): the FL_DUMP twin
+    of its shipped schedule stores the S^T it feeds its softmax, its in-register int8 Q operand
+    (quantised with the head slice's scale) and that scale; each equals the oracle's
+    quantize_heads_pt / qk_int32 bit for bit, and its O equals flash_solve's bit for bit."""
+    from quantizedmha_amd import torch_ext
+    dm = h * d
+    Q, K, V = rand_inputs(70 + N + h, B, N, dm)
+    Q, K, V = (x.reshape(B, N, dm) for x in (Q, K, V))
+    Q[0, 5, :] *= 9.0  # an outlier row sets its whole head slice's scale
+    K[-1, N - 1, :d] = 0.0
+    tq, tk, tv = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (Q, K, V))
+    O, S, Qi, sQ = torch_ext.debug_fa_int8_dump(tq, tk, tv, dm, h, per_tensor=True)
+    ref_O = torch_ext.flash_solve(tq, tk, tv, dm, h, kernel="fa_tc_int8_pt")
+    torch.cuda.synchronize()
+    assert torch.equal(O, ref_O)
+    for b, k in heads or [(b, k) for b in range(B) for k in range(h)]:
+        Qi_ref, sq_ref = oracle_mod.quantize_heads_pt(Q[b], dm, h)
+        Ki_ref, _ = oracle_mod.quantize_heads_pt(K[b], dm, h)
+        assert np.array_equal(Qi[b, k].cpu().numpy(), Qi_ref[0, k]), (b, k)
+        assert np.all(sQ[b, k].cpu().numpy() == sq_ref[0, k]), (b, k)
+        S_ref = oracle_mod.qk_int32(Qi_ref[0, k], Ki_ref[0, k])
+        assert np.array_equal(S[b, k].cpu().numpy(), S_ref), (b, k)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("case", ["medium", "large"])
 def test_variant_vs_reference_golden(dev, oracle_mod, variant, case):
