@@ -385,6 +385,9 @@ __global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) voi
 // K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
 // barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
 // ---------------------------------------------------------------------------------------
+#ifndef QMHA_PT_D128_SCHED
+#define QMHA_PT_D128_SCHED 0
+#endif
 // fa_tc_int8_pt's MFMA placement: the j-th (j < 2) MFMA issued after VALU region s (s < 6) of an
 // iteration, -1 for none; op 2m + ks = P@V of d-block m, k-step ks (tile t-1), op 8 + ks = Q@K^T
 // k-step ks (tile t+1).  P@V(m, 1) trails P@V(m, 0) by >= 2 slots; Q@K^T sits mid-iteration so
@@ -393,7 +396,9 @@ __host__ __device__ constexpr int pt_slot_op(int D, int s, int j) {
     constexpr int d32[6][2] = {{0, -1}, {-1, -1}, {1, -1}, {8, -1}, {-1, -1}, {-1, -1}};
     constexpr int d64[6][2] = {{0, -1}, {2, -1}, {1, -1}, {8, -1}, {9, -1}, {3, -1}};
     constexpr int d128[6][2] = {{0, 2}, {4, 6}, {1, 3}, {8, 9}, {10, 11}, {5, 7}};
-    return D == 32 ? d32[s][j] : D == 64 ? d64[s][j] : d128[s][j];
+    // A/B (QMHA_PT_D128_SCHED=1): every Q@K^T step in its own slot, beside a P@V
+    constexpr int d128b[6][2] = {{0, 8}, {2, 9}, {4, 10}, {6, 11}, {1, 3}, {5, 7}};
+    return D == 32 ? d32[s][j] : D == 64 ? d64[s][j] : (QMHA_PT_D128_SCHED ? d128b[s][j] : d128[s][j]);
 }
 
 template <int N>
