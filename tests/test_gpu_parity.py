@@ -489,6 +489,25 @@ def _slices_vs_oracle(oracle_fn, Q, K, V, out, d, slices, nthreads=16):
 C_SLICES = [(b, (7 * b + 3) % 16) for b in range(16)]
 
 
+@pytest.mark.parametrize("variant", INT8_VARIANTS)
+@pytest.mark.parametrize("B,H,d", [(16, 8, 128), (16, 32, 32)])
+def test_int8_other_head_sizes_bench_shapes(dev, oracle_mod, variant, B, H, d):
+    """The d = 128 and d = 32 shapes DESIGN.md quotes timings for (N = 4096, B16 H8 d128 and
+    B16 H32 d32, both int8 variants): 8 (batch, head) slices spread over the grid against the
+    oracle at the N >= 2048 bound, all outputs finite."""
+    from quantizedmha_amd import torch_ext
+    N = 4096
+    g = torch.Generator(device=dev).manual_seed(d)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel=variant)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    slices = [(2 * i, (5 * i + 1) % H) for i in range(8)]
+    oracle_fn = oracle_mod.fa_int8 if variant == "fa_tc_int8_b" else oracle_mod.fa_int8_pt
+    got, ref = _slices_vs_oracle(oracle_fn, Q, K, V, out, d, slices)
+    assert_parity(variant, got, ref)
+
+
 def test_full_baseline_config_sampled_heads(dev, oracle_mod):
     """BASELINE C4 (B16 H16 N4096 d64, int8): the whole call on the GPU; 16 (batch, head) slices
     spread across the XCD remap against the oracle, every row's convexity (all-positive V =>
