@@ -1081,6 +1081,8 @@ __global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL
     // in the region before their slot's predecessor (two slots ahead).  P@V accumulates straight
     // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
     // P@V of t-2 has), so no MFMA result is waited on.
+    // iter_pt forms the exponent as fma(accumulator bits, c', -Kn): the MAGIC-biased accumulator and KFOLD
+    static_assert(!PT || (MAGIC && KFOLD), "FL_PT needs FL_MAGIC | FL_KFOLD");
     float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
     auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
