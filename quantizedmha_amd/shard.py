@@ -81,7 +81,9 @@ def solve_shard_gather(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_mode
     travels on its own link, and nothing is staged, padded or reordered: uneven shards just send
     fewer rows.  Chunk c's exchange is issued right after chunk c's kernels are enqueued, so it
     runs on the collective stream while chunk c+1 computes; chunk boundaries (chunks of the
-    largest shard's width) are the same on every rank, so sends and receives pair up.
+    largest shard's width) are the same on every rank, so sends and receives pair up.  Peers are
+    addressed by their rank INSIDE `group` (P2POp's group_peer; its positional `peer` is a global
+    rank), so a subgroup whose members are not global ranks 0..W-1 exchanges correctly.
 
     solve_fn (CPU tests: the oracle) returns a new tensor that is copied into the slab; the
     default HIP path writes in place."""
@@ -119,10 +121,10 @@ def solve_shard_gather(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, d_mode
             if p == rank:
                 continue
             if n > 0:
-                ops.append(dist.P2POp(dist.isend, mine, p, group))
+                ops.append(dist.P2POp(dist.isend, mine, group=group, group_peer=p))
             n_p = max(0, min(c1, pe - ps) - c0)
             if n_p > 0:
-                ops.append(dist.P2POp(dist.irecv, out[ps + c0:ps + c0 + n_p], p, group))
+                ops.append(dist.P2POp(dist.irecv, out[ps + c0:ps + c0 + n_p], group=group, group_peer=p))
         if ops:
             works.extend(dist.batch_isend_irecv(ops))
     for w in works:

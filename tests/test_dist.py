@@ -97,6 +97,46 @@ def test_shard_gloo(oracle_mod, tmp_path, world, B, kernel):
         assert torch.equal(out, ref), key  # sharding is exact: the same per-sequence computation
 
 
+def _subgroup_worker(rank, world, port, B, result_path):
+    """World-4 job; ranks 1 and 3 form a subgroup and run the batch-shard path on it (round-3
+    ADVICE: P2POp peers must be ranks inside the group, not global ranks)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group([1, 3])  # every rank takes part in creating the group
+        if rank in (1, 3):
+            from oracle import oracle
+            Q, K, V = _inputs(B, 64, 128, seed=11)
+            r_sub = dist.get_rank(sub)
+            start, stop = batch_shard(B, r_sub, 2)
+            sh = [t[start:stop].clone() for t in (Q, K, V)]
+            outs = {f"chunks{c}": solve_sharded(*sh, 128, 2, "fa_tc_int8_b", batch=B, chunks=c, group=sub,
+                                                 solve_fn=_oracle_solve(oracle)) for c in (1, 2)}
+            outs["full"] = solve_sharded(Q, K, V, 128, 2, "fa_tc_int8_b", group=sub, solve_fn=_oracle_solve(oracle))
+            own = _oracle_solve(oracle)(*sh, 128, 2, "fa_tc_int8_b")
+            outs["gather_outputs"] = gather_outputs(own, B, group=sub)
+            torch.save(outs, f"{result_path}.{rank}")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_gloo_subgroup(oracle_mod, tmp_path):
+    """The `group=` argument with a subgroup whose members are not global ranks 0..W-1 (ranks 1 and 3
+    of a world-4 job): both members end with the full, exact result (even and uneven shards)."""
+    for B in (4, 5):
+        path = str(tmp_path / f"sub{B}.pt")
+        mp.start_processes(_subgroup_worker, args=(4, _free_port(), B, path), nprocs=4, join=True,
+                           start_method="spawn")
+        Q, K, V = _inputs(B, 64, 128, seed=11)
+        ref = _oracle_solve(oracle_mod)(Q, K, V, 128, 2, "fa_tc_int8_b")
+        for r in (1, 3):
+            res = torch.load(f"{path}.{r}", weights_only=True)
+            for key, out in res.items():
+                assert out.shape == (B, 64, 128), (r, key)
+                assert torch.equal(out, ref), (B, r, key)
+
+
 def test_bench_spawns_ranks_dry_run():
     """`python bench.py --gpus 2` with no launcher spawns its own two ranks (torch.distributed.run,
     127.0.0.1); --dry-run runs the plumbing on CPU/gloo.  Rank 0 prints one JSON line with
