@@ -57,7 +57,8 @@ enum {
  * columns [k*d, (k+1)*d), d = d_model / h.  output is fully overwritten.
  * Blocking: the result is complete on return (reference launchers.h:64).  Scratch is
  * owned by the library.  Preconditions (the reference asserts N % 32 on the device,
- * fa_tc_int8_b.cu:422-423): N % 32 == 0, d_model == h*d, d in {32, 64, 128}.  The
+ * fa_tc_int8_b.cu:422-423): N % 32 == 0, d_model == h*d, d % 32 == 0 (config.h:32) and d <= 256
+ * (fa_tc_int8_pt, the per-tensor mode with no reference counterpart: d in {32, 64, 128}).  The
  * reference's d is a compile-time constant (config.h:28); here it is a runtime value.
  * On a violated precondition or HIP error `solve` prints one line to stderr and returns
  * (the reference returns void and ignores errors).

@@ -54,13 +54,21 @@ int check_shape(const void* Q, const void* K, const void* V, const void* O, int 
         return QMHA_ERR_INVALID;
     }
     const int D = d_model / h;
-    if (D != 32 && D != 64 && D != 128) {  // config.h:32 requires d % 32 == 0
-        g_last_error = "head size d = d_model/h must be 32, 64 or 128";
-        return QMHA_ERR_NOSYS;
-    }
     if (variant < QMHA_FA || variant > QMHA_FA_TC_INT8_PT) {
         g_last_error = "unknown variant";
         return QMHA_ERR_INVALID;
+    }
+    if (D % 32 != 0) {  // config.h:32: static_assert(d % 32 == 0)
+        g_last_error = "head size d = d_model/h must be a multiple of 32";
+        return QMHA_ERR_INVALID;
+    }
+    if (D > 256) {  // the reference has no upper bound; here the int8 magic-biased accumulator's range
+        g_last_error = "head size d = d_model/h above 256 is not built";
+        return QMHA_ERR_NOSYS;
+    }
+    if (variant == QMHA_FA_TC_INT8_PT && D != 32 && D != 64 && D != 128) {  // no reference counterpart
+        g_last_error = "fa_tc_int8_pt is built for d = 32, 64, 128 only";
+        return QMHA_ERR_NOSYS;
     }
     if ((size_t)B * N * d_model > (size_t)INT32_MAX * 4) {
         g_last_error = "tensor too large";
@@ -374,6 +382,10 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
         g_last_error = "bad scales pointer or layout";
         return QMHA_ERR_INVALID;
     }
+    if (layout == 2 && D != 32 && D != 64 && D != 128) {  // the per-tensor mode's quantiser
+        g_last_error = "layout 2 (per-tensor scales) is built for d = 32, 64, 128 only";
+        return QMHA_ERR_NOSYS;
+    }
     if (layout == 2) {  // per-tensor (head-slice) scales: group absmax pass + quantisation pass
         const size_t need = qmha::align_up((size_t)3 * B * h * (N / 32) * sizeof(float), 256);
         void* ws = nullptr;
@@ -429,8 +441,8 @@ int qmha_debug_fa_int8_dump(const float* Q, const float* K, const float* V, floa
     int D = 0;
     int st = check_shape(Q, K, V, O, B, N, d_model, h, QMHA_FA_TC_INT8_B, &D);
     if (st != QMHA_OK) return st;
-    if (!S || !Qi || !sQ || N < 64) {
-        g_last_error = "debug dump: needs S/Qi/sQ buffers and N >= 64 (the pipelined kernel)";
+    if (!S || !Qi || !sQ || ((D == 32 || D == 64 || D == 128) && N < 64)) {
+        g_last_error = "debug dump: needs S/Qi/sQ buffers and, at d = 32 / 64 / 128, N >= 64 (the pipelined kernel)";
         return QMHA_ERR_INVALID;
     }
     const size_t need = qmha::int8_workspace_bytes(B, N, h, D);

@@ -84,6 +84,32 @@ __host__ __device__ constexpr int slot_of_kv_f16(int kv) {
     return 16 * (kv >> 4) + 8 * ((kv >> 2) & 1) + (kv & 3) + 4 * ((kv >> 3) & 1);
 }
 
+// LDS layout of a row of RB bytes read as 16-byte chunks by ds_read_b128 with one row per lane
+// (rows 0..31 of a 32 x RB operand).  swz_pos<RB>(row, c) = the LDS chunk slot holding source
+// chunk c of `row`; swz_src<RB>(row, j) = the source chunk stored in slot j.  Power-of-two chunk
+// counts (d = 32 / 64 / 128 / 256): an XOR swizzle, conflict-free per 16-lane group (an
+// involution, so both directions are the same).  Other counts (d = 96 / 160 / 192 / 224): a
+// rotation by the row's bank-row index (a bijection for any count).
+template <int RB>
+__device__ __forceinline__ int swz_rot(int row) {
+    constexpr int rows_per_bankrow = 256 / RB >= 1 ? 256 / RB : 1;
+    constexpr int cpr = RB / 16;
+    if constexpr ((cpr & (cpr - 1)) == 0) return (row / rows_per_bankrow) & (cpr - 1);
+    else return (row / rows_per_bankrow) % cpr;
+}
+template <int RB>
+__device__ __forceinline__ int swz_pos(int row, int c) {
+    constexpr int cpr = RB / 16;
+    if constexpr ((cpr & (cpr - 1)) == 0) return c ^ swz_rot<RB>(row);
+    else return (c + swz_rot<RB>(row)) % cpr;
+}
+template <int RB>
+__device__ __forceinline__ int swz_src(int row, int j) {
+    constexpr int cpr = RB / 16;
+    if constexpr ((cpr & (cpr - 1)) == 0) return j ^ swz_rot<RB>(row);
+    else return (j + cpr - swz_rot<RB>(row)) % cpr;
+}
+
 // --------------------------------------------------------------------------
 // cross-lane helpers (wave64)
 // --------------------------------------------------------------------------

@@ -20,11 +20,6 @@ namespace qmha {
 
 static constexpr float kLog2eH = 1.4426950408889634f;
 
-template <int RB>
-__device__ __forceinline__ int chunk_swz_h(int row) {
-    constexpr int rpb = 256 / RB >= 1 ? 256 / RB : 1;
-    return (row / rpb) & (RB / 16 - 1);
-}
 
 // ---------------------------------------------------------------------------------------
 // Main kernel: K/V staged by LDS-DMA (global_load_lds, swizzled source / linear LDS image),
@@ -35,10 +30,11 @@ __device__ __forceinline__ int chunk_swz_h(int row) {
 // not wait on their LDS reads
 // F16_UNROLL: two stages per loop trip, so each stage's LDS buffer is a compile-time constant and
 // every operand read is a base register plus an immediate (no per-tile address arithmetic)
-enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16 };
+// F16_LB1: a one-wave-per-SIMD register budget (VGPRs + AGPRs) for d > 128, whose O alone is d/2 VGPRs
+enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16, F16_LB1 = 32 };
 
 template <int D, int WAVES, int SG, int FL>
-__global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f16_v2_kernel(
+__global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 1 : 2)) void qmha_fa_f16_v2_kernel(
     const float* __restrict__ Qf, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     QMHA_ENABLE_AGPR_MFMA();
@@ -102,14 +98,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
-        const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ chunk_swz_h<RB>(row);
+        const int row = idx / (RB / 16), cc = swz_src<RB>(row, idx % (RB / 16));
         koff[jj] = row * RB + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
         const int grp = idx / (4 * D), w = idx % (4 * D);
-        const int d = w >> 2, cv = (w & 3) ^ chunk_swz_h<64>(d);
+        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
     }
     auto issue = [&](int buf, int st) {
@@ -134,7 +130,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
         const int krow = gi * 32 + col;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((2 * ks + half) ^ chunk_swz_h<RB>(krow)));
+            const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * swz_pos<RB>(krow, 2 * ks + half));
             s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kop, qop[ks], s, 0, 0, 0);
         }
         return s;
@@ -149,7 +145,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
                 for (int ks = 0; ks < 2; ++ks) {
                     const int d = 32 * m + col;
                     vpre[m][ks] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 +
-                                                                16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                                                                16 * swz_pos<64>(d, 2 * ks + half));
                 }
         }
         float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);  // max3 chain
@@ -182,7 +178,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : 2) void qmha_fa_f1
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const v8h vop = (FL & F16_VPRE) ? vpre[m][ks]
-                                                : *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz_h<64>(d)));
+                                                : *reinterpret_cast<const v8h*>(vr + 16 * swz_pos<64>(d, 2 * ks + half));
                 o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[ks], o[m], 0, 0, 0);
             }
         }
@@ -337,8 +333,13 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
     // 1.71 ms for the interleaved-pair kernel at B16 H16 N4096 d64), 8-wave workgroups: each LDS-DMA
     // stage is shared by 8 waves (one 1-KiB piece per wave and tile instead of two) at the same
     // occupancy (r03m: main -2.1 % against 4-wave workgroups, 16 waves +0 %, profiles/r03/ab/f16_wg).
-    // d = 128 keeps 4-wave workgroups: its 199 VGPRs do not fit the 8-wave register budget (111 spills)
-    return fa_f16_v2_launch<D, (D <= 64 ? QMHA_F16_WAVES : 4), 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
+    // d = 128 keeps 4-wave workgroups: its 199 VGPRs do not fit the 8-wave register budget (111 spills).
+    // Other head sizes (d % 32 == 0, include/config.h:32): 4-wave workgroups, the V operands read at
+    // their MFMA, a 2-wave budget at d = 96 and 1 wave above d = 128
+    if constexpr (D == 32 || D == 64 || D == 128)
+        return fa_f16_v2_launch<D, (D <= 64 ? QMHA_F16_WAVES : 4), 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
+    else
+        return fa_f16_v2_launch<D, 4, 2, F16_UNROLL | (D > 128 ? F16_LB1 : 0)>(w, Qf, O, B, N, H, d_model, stream);
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,
@@ -347,6 +348,11 @@ hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, 
         case 32: return fa_f16_d<32>(w, Qf, O, B, N, H, d_model, stream);
         case 64: return fa_f16_d<64>(w, Qf, O, B, N, H, d_model, stream);
         case 128: return fa_f16_d<128>(w, Qf, O, B, N, H, d_model, stream);
+        case 96: return fa_f16_d<96>(w, Qf, O, B, N, H, d_model, stream);
+        case 160: return fa_f16_d<160>(w, Qf, O, B, N, H, d_model, stream);
+        case 192: return fa_f16_d<192>(w, Qf, O, B, N, H, d_model, stream);
+        case 224: return fa_f16_d<224>(w, Qf, O, B, N, H, d_model, stream);
+        case 256: return fa_f16_d<256>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

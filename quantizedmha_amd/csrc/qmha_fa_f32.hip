@@ -200,7 +200,7 @@ __global__ __launch_bounds__(NT) void qmha_fa_f32_v3_kernel(const float* __restr
 // O = O*alpha + PV, guard 1e-10).
 // ---------------------------------------------------------------------------------------
 template <int D>
-__global__ __launch_bounds__(256, D == 128 ? 2 : 3) void qmha_fa_f32_mfma_kernel(
+__global__ __launch_bounds__(256, D <= 64 ? 3 : (D <= 128 ? 2 : 1)) void qmha_fa_f32_mfma_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, float* __restrict__ O,
     int N, int H, int d_model, float inv_sqrt_d) {
     constexpr int HD = D / 2, MB = D / 32;
@@ -346,6 +346,11 @@ hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* 
             case 32: return fa_f32_mfma<32>(Q, K, V, O, B, N, H, d_model, stream);
             case 64: return fa_f32_mfma<64>(Q, K, V, O, B, N, H, d_model, stream);
             case 128: return fa_f32_mfma<128>(Q, K, V, O, B, N, H, d_model, stream);
+            case 96: return fa_f32_mfma<96>(Q, K, V, O, B, N, H, d_model, stream);
+            case 160: return fa_f32_mfma<160>(Q, K, V, O, B, N, H, d_model, stream);
+            case 192: return fa_f32_mfma<192>(Q, K, V, O, B, N, H, d_model, stream);
+            case 224: return fa_f32_mfma<224>(Q, K, V, O, B, N, H, d_model, stream);
+            case 256: return fa_f32_mfma<256>(Q, K, V, O, B, N, H, d_model, stream);
             default: return hipErrorInvalidValue;
         }
     }
@@ -359,12 +364,17 @@ hipError_t launch_fa_f32(const float* Q, const float* K, const float* V, float* 
         }
     }
 #endif
-    // fa: the scalar kernel, 4 rows per thread (128 rows per workgroup; 64 at d = 128, whose
-    // Q / K / V / P tiles would otherwise take 121 KiB of LDS)
+    // fa: the scalar kernel, 4 rows per thread (128 rows per workgroup; 64 above d = 64, whose
+    // Q / K / V / P tiles would otherwise take up to 280 KiB of LDS: 146 KiB at d = 256)
     switch (D) {
         case 32: return fa_f32_v3<32, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
         case 64: return fa_f32_v3<64, 4, 256>(Q, K, V, O, B, N, H, d_model, stream);
         case 128: return fa_f32_v3<128, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 96: return fa_f32_v3<96, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 160: return fa_f32_v3<160, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 192: return fa_f32_v3<192, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 224: return fa_f32_v3<224, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
+        case 256: return fa_f32_v3<256, 2, 256>(Q, K, V, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -216,6 +216,105 @@ __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
 }
 
 
+// ---------------------------------------------------------------------------------------
+// Every other head size the reference accepts (d % 32 == 0, include/config.h:32; d = 96, 160, 192,
+// 224, 256): one wave per (tensor, bh, 32-row group) as above, with a lane map that works for any
+// d -- lane l holds the 16-byte quads l, l + 64, ... of the group's 32 x d block (row = q / (d/4)),
+// coalesced along each row -- and the V^T operand written through the wave's LDS tile element by
+// element (2-byte / 1-byte scattered writes; these head sizes are not the tuned path).
+// QUANT: the int8 quantiser (fa_tc_int8_b.cu:33-152) -- rows as int8, V as f16-valued integers
+// (VMODE 1) or int8 (VMODE 0); otherwise the fp16 conversion (fa_tc_v1a.cu:300-330) -- rows and V
+// as f16 (RNE).
+// ---------------------------------------------------------------------------------------
+template <int D, int VMODE, bool QUANT>
+__global__ __launch_bounds__(256) void qmha_prepass_any_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, void* __restrict__ Qo,
+    void* __restrict__ Ko, void* __restrict__ Vout, float* __restrict__ sQ, float* __restrict__ sK,
+    float* __restrict__ sV, int N, int H, int d_model, int total_groups, int first_tensor) {
+    constexpr int C4 = D / 4, NQ = D / 8;                 // quads per row, quads per lane
+    constexpr int VB = (VMODE == 1 || !QUANT) ? 64 : 32;  // V^T operand bytes per d-row (32 slots)
+    __shared__ __attribute__((aligned(16))) char vtr[4][D * 64];
+    const int tensor = blockIdx.y + first_tensor;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + wave;
+    if (item >= total_groups) return;  // wave-uniform
+    const int G = N / QMHA_GROUP;
+    const int bh = item / G, g = item % G;
+    const int b = bh / H, k = bh % H;
+    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
+    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D;
+    v4f x[NQ];
+    float amax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const int q = i * 64 + lane, row = q / C4, c4 = q % C4;
+        x[i] = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)row * d_model + 4 * c4));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
+    }
+    float sc = 1.0f, inv = 1.0f;
+    if constexpr (QUANT) {
+        sc = qmha_scale_from_absmax(wave_max64(amax));  // fa_tc_int8_b.cu:104
+        inv = 1.0f / sc;                                // :106
+        float* s_out = tensor == 0 ? sQ : (tensor == 1 ? sK : sV);
+        if (lane == 0 && s_out) s_out[(size_t)bh * G + g] = sc;
+    }
+    if (tensor < 2) {  // rows [bh][N][D]
+        char* dst = static_cast<char*>(tensor == 0 ? Qo : Ko);
+        if (!dst) return;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            const int q = i * 64 + lane, row = q / C4, c4 = q % C4;
+            const size_t e0 = ((size_t)bh * N + (size_t)g * QMHA_GROUP + row) * D + 4 * c4;
+            if constexpr (QUANT) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(x[i][c], inv)) << (8 * c);
+                *reinterpret_cast<uint32_t*>(dst + e0) = w;
+            } else {
+                v4h hv;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) hv[c] = (_Float16)x[i][c];  // RNE (= __float2half)
+                *reinterpret_cast<v4h*>(dst + 2 * e0) = hv;
+            }
+        }
+        return;
+    }
+    // V: the [D][32 slots] V^T operand block of this group through the wave's LDS tile
+    char* T = vtr[wave];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const int q = i * 64 + lane, row = q / C4, c4 = q % C4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int d = 4 * c4 + c;
+            if constexpr (!QUANT)
+                *reinterpret_cast<_Float16*>(T + d * 64 + 2 * slot_of_kv_f16(row)) = (_Float16)x[i][c];
+            else if constexpr (VMODE == 1)
+                *reinterpret_cast<_Float16*>(T + d * 64 + 2 * slot_of_kv_f16(row)) = (_Float16)qmha_quant_i8(x[i][c], inv);
+            else
+                *reinterpret_cast<int8_t*>(T + d * 32 + slot_of_kv_i8(row)) = (int8_t)qmha_quant_i8(x[i][c], inv);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    char* dst = static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(VB * D);
+    constexpr int LINES = D * VB / 16;
+#pragma unroll
+    for (int u = lane; u < LINES; u += 64) *reinterpret_cast<v4i*>(dst + 16 * u) = *reinterpret_cast<const v4i*>(T + 16 * u);
+}
+
+template <int D, int VMODE, bool QUANT>
+static hipError_t prepass_any_d(const float* Q, const float* K, const float* V, void* Qo, void* Ko, void* Vout, float* sQ,
+                                float* sK, float* sV, int B, int N, int H, int d_model, int first_tensor, int num_tensors,
+                                hipStream_t stream) {
+    const int total = B * H * (N / QMHA_GROUP);
+    dim3 grid((total + 3) / 4, num_tensors > 0 ? num_tensors : 3 - first_tensor);
+    hipLaunchKernelGGL((qmha_prepass_any_kernel<D, VMODE, QUANT>), grid, dim3(256), 0, stream, Q, K, V, Qo, Ko, Vout, sQ, sK,
+                       sV, N, H, d_model, total, first_tensor);
+    return hipGetLastError();
+}
+
 template <int D>
 static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, void* vout,
                                int v_mode, int B, int N, int H, int d_model, int first_tensor, int num_tensors,
@@ -288,6 +387,14 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
         case 32: return quant_int8_d<32>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
         case 64: return quant_int8_d<64>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
         case 128: return quant_int8_d<128>(Q, K, V, w, vout, v_mode, B, N, H, d_model, first_tensor, num_tensors, stream);
+#define QMHA_CASE(d)                                                                                                      \
+    case d:                                                                                                               \
+        return v_mode == 0 ? prepass_any_d<d, 0, true>(Q, K, V, w.Qi, w.Ki, vout, w.sQ, w.sK, w.sV, B, N, H, d_model,     \
+                                                       first_tensor, num_tensors, stream)                                \
+                           : prepass_any_d<d, 1, true>(Q, K, V, w.Qi, w.Ki, vout, w.sQ, w.sK, w.sV, B, N, H, d_model,     \
+                                                       first_tensor, num_tensors, stream);
+        QMHA_CASE(96) QMHA_CASE(160) QMHA_CASE(192) QMHA_CASE(224) QMHA_CASE(256)
+#undef QMHA_CASE
         default: return hipErrorInvalidValue;
     }
 }
@@ -309,6 +416,10 @@ hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, co
         case 32: return convert_f16_d<32>(Q, K, V, w, B, N, H, d_model, stream);
         case 64: return convert_f16_d<64>(Q, K, V, w, B, N, H, d_model, stream);
         case 128: return convert_f16_d<128>(Q, K, V, w, B, N, H, d_model, stream);
+#define QMHA_CASE(d) \
+    case d: return prepass_any_d<d, 1, false>(Q, K, V, w.Qh, w.Kh, w.Vt, nullptr, nullptr, nullptr, B, N, H, d_model, 1, -1, stream);
+        QMHA_CASE(96) QMHA_CASE(160) QMHA_CASE(192) QMHA_CASE(224) QMHA_CASE(256)
+#undef QMHA_CASE
         default: return hipErrorInvalidValue;
     }
 }

@@ -77,6 +77,9 @@ def test_host_side_queries(built):
 @pytest.mark.parametrize("args,err", [
     ((1, 100, 128, 2, 2), "N must be a multiple of 32"),
     ((1, 128, 130, 2, 2), "head size"),
+    ((1, 128, 96, 2, 2), "multiple of 32"),   # d = 48 (config.h:32)
+    ((1, 128, 1024, 2, 2), "above 256"),      # d = 512
+    ((1, 128, 192, 2, 5), "d = 32, 64, 128"),  # d = 96 in the per-tensor mode
     ((1, 128, 128, 3, 2), "divisible"),
     ((1, 128, 128, 2, 7), "unknown variant"),
     ((0, 128, 128, 2, 2), "positive"),
@@ -164,20 +167,31 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     for name, d, rest in stubs:
         if name.startswith("qmha_gemm"):
             continue
-        m = re.match(r"Li(\d+)ELi(\d+)E", rest) if name == "qmha_fa_int8_pipe_kernel" else None
-        if m and int(m.group(2)) & 1048576:  # FL_PT: the fa_tc_int8_pt variant's own instance
+        if name == "qmha_fa_int8_pipe_kernel":  # <D, WAVES, FL>
+            m, fl = re.match(r"Li(\d+)ELi(\d+)E", rest), 2
+        elif name == "qmha_fa_int8_kernel":  # <D, FL> (the one-tile kernel: N = 32, and d outside 32/64/128)
+            m, fl = re.match(r"Li(\d+)E", rest), 1
+        else:
+            m = None
+        if m and int(m.group(fl)) & 1048576:  # FL_PT: the fa_tc_int8_pt variant's own instance
             name += "[pt]"
-        if m and int(m.group(2)) & 256:  # FL_DUMP: the test-hook twin of the production instance
-            dumps.append((name, d, rest.replace(f"ELi{m.group(2)}E", f"ELi{int(m.group(2)) & ~256}E", 1)))
+        if m and int(m.group(fl)) & 256:  # FL_DUMP: the test-hook twin of the production instance
+            f = m.group(fl)
+            twin = rest.replace(f"Li{f}E", f"Li{int(f) & ~256}E", 1) if fl == 1 else \
+                rest.replace(f"ELi{f}E", f"ELi{int(f) & ~256}E", 1)
+            dumps.append((name, d, twin))
             continue
         per.setdefault((name, d), set()).add(rest)
-    assert len(dumps) == 6, dumps  # per-block and per-tensor, d = 32 / 64 / 128
+    # per-block d = 32 / 64 / 128 (pipelined) and 96 / 160 / 192 / 224 / 256 (one-tile kernel),
+    # per-tensor d = 32 / 64 / 128
+    assert len(dumps) == 11, dumps
     for name, d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
         assert per[(name, d)] == {twin}, (name, d, twin)
     assert per, syms[:2000]
     for (name, d), inst in per.items():
-        # the V layout and the per-tensor mode are template arguments of the quantiser
-        limit = 3 if name == "qmha_quant_int8_kernel" else 1
+        # the V layout and the per-tensor mode are template arguments of the quantiser; the any-d
+        # pre-pass is instantiated for the int8 V layouts and the fp16 conversion
+        limit = 3 if name in ("qmha_quant_int8_kernel", "qmha_prepass_any_kernel") else 1
         assert len(inst) <= limit, (name, d, sorted(inst))
     blob = open(path, "rb").read()
     for env in (b"QMHA_INT8_CFG", b"QMHA_F16_CFG", b"QMHA_F32_CFG", b"QMHA_OVERLAP_CHUNKS", b"QMHA_INT8_ABL"):
@@ -193,7 +207,7 @@ def test_fa_scalar_kernel_has_no_matrix_core_instructions(built):
     funcs = {f.split("\n", 1)[0]: f for f in re.split(r"\n(?=[0-9a-f]+ <)", asm)}
     scalar = [k for k in funcs if "qmha_fa_f32_v3_kernel" in k]
     mfma = [k for k in funcs if "qmha_fa_f32_mfma_kernel" in k]
-    assert len(scalar) == 3 and len(mfma) == 3, (scalar, mfma)  # d = 32, 64, 128
+    assert len(scalar) == 8 and len(mfma) == 8, (scalar, mfma)  # d = 32, 64, ..., 256
     for k in scalar:
         assert "v_mfma" not in funcs[k] and "v_fma_f32" in funcs[k], k
     for k in mfma:

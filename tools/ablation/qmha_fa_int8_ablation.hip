@@ -1,0 +1,1624 @@
+// qmha_fa_int8.hip -- fused INT8 FlashAttention-2 forward for gfx950 (MI355X).
+//
+// Drop-in for the reference's fa_tc_int8_b (mha_kernels/fa_tc_int8_b.cu:408-609) with its
+// *intended* numerics:
+//   per 32-row group of Q, K, V:  s = max(absmax/127, 1e-8), x_i8 = clamp(rint(x * (1/s)))
+//   S = Qi Ki^T (int32, exact)        -> scores = S * sQ * sK / sqrt(d)
+//   online softmax per 32-key tile, m0 = 0 -> p = exp(scores - m), l = alpha*l + sum(p)
+//   per 32x32 tile P: sP = max(max p / 127, 1e-8), Pi = rint(p / sP)
+//   O = alpha*O + (Pi Vi) * sP * sV,   out = O / l  (0 if l <= 1e-20)
+//
+// Two launches per call:
+//   1. qmha_quant_int8_kernel (qmha_prepass.hip): reads fp32 K/V once; writes int8 K rows per head and the
+//      quantised V integers in the MFMA V^T operand order, one fp32 scale per group.
+//      Bit-identical to the reference quantiser (same fp32 ops, RNE rounding).  (With Q too
+//      for qmha_quantize_int8 and the int32 Q@K^T test hook.)
+//   2. qmha_fa_int8_pipe_kernel (d = 64; qmha_fa_int8_kernel otherwise): one workgroup = 4
+//      waves = 128 query rows of one head; each wave owns one 32-row Q group, quantises it
+//      in registers (the same arithmetic) and sweeps all KV groups.  K/V tiles stream
+//      L2 -> LDS by LDS-DMA (XOR-swizzled image, conflict-free ds_read_b128).  Both products
+//      use swapped operands (S^T = K Q^T, O^T = V^T P^T) so every query's statistics are
+//      lane-local and P^T feeds the second MFMA from registers.
+//        Q@K^T: v_mfma_i32_32x32x32_i8, exact int32 scores.
+//        P@V  : the int8-valued operands Pi in [0,127], Vi in [-128,127] run on
+//               v_mfma_f32_32x32x16_f16.  Both are exact in f16, every product and every
+//               partial sum (|sum| <= 32*127*128 < 2^24) is exact in the fp32 accumulator,
+//               so the result equals the reference's int32 (Pi Vi) bit for bit -- but it
+//               arrives as fp32, saving the 32 int->float conversions per lane per tile.
+//      Software pipelining: P@V of tile t-1 and Q@K^T of tile t+1 are issued between the
+//      softmax chunks of tile t.
+#include "qmha_common.hpp"
+#include "qmha_kernels.hpp"
+
+#include <cstdlib>
+#include <type_traits>
+
+namespace qmha {
+
+// log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
+static constexpr float kLog2e = 1.4426950408889634f;
+
+// LDS XOR swizzle for a row of RB bytes read as 16-byte chunks by ds_read_b128 with one
+// row per lane (rows 0..31 of a 32x32 operand): conflict-free per 16-lane group.
+template <int RB>
+__device__ __forceinline__ int chunk_swz(int row) {
+    constexpr int rows_per_bankrow = 256 / RB >= 1 ? 256 / RB : 1;
+    constexpr int cpr = RB / 16;
+    return (row / rows_per_bankrow) & (cpr - 1);
+}
+
+// In-kernel Q quantisation (fa_tc_int8_b.cu:33-152, the pre-pass arithmetic) straight into
+// the Q^T MFMA operand: lane (col, half) loads the D/2 values of query row `col` it feeds to
+// the i8 MFMA (bytes [32 s + 16 half, +16) of every k-step s), the wave reduces the group's
+// absmax.  Returns the group scale sQ.  Saves the pre-pass a third of its HBM traffic.
+// slice_sc > 0: the per-tensor mode's head-slice scale (no group absmax)
+template <int D>
+__device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, int half, v4i (&qop)[D / 32],
+                                                 float slice_sc = 0.0f) {
+    constexpr int KS = D / 32;
+    v4f x[KS][4];
+    float amax = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            x[s][c4] = *reinterpret_cast<const v4f*>(row + 32 * s + 16 * half + 4 * c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(x[s][c4][e]));
+        }
+    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));
+    const float inv = 1.0f / sc;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w |= ((uint32_t)(uint8_t)qmha_quant_i8(x[s][c4][e], inv)) << (8 * e);
+            qop[s][c4] = (int)w;
+        }
+    return sc;
+}
+
+// ---------------------------------------------------------------------------------------
+// Main kernel.
+//
+// One workgroup = WAVES waves; each wave owns QPW 32-row Q groups (= Q quantisation groups)
+// of one head and sweeps all KV groups of that head.  Per 32-key tile and Q group:
+//   S^T = K Q^T            v_mfma_i32_32x32x32_i8 (int32, exact; K operand shared by the
+//                          wave's Q groups)
+//   online softmax         lane-local per query (swapped product), m0 = 0
+//   P tile scale sP        max over the 32x32 tile (DPP + permlane16)
+//   Pi = rint(p / sP)      magic-number RNE, packed to f16
+//   O^T += V^T P^T         v_mfma_f32_32x32x16_f16 on exact f16 integers (= the int32 product)
+// FL (build-time flags):
+//   FL_MAGIC    the Q@K^T chain starts from the bits of 1.5*2^23, so every int32 accumulator lane
+//               reads as the float 1.5*2^23 + S (exact: |S| <= 2^21 for d <= 128); one packed
+//               subtract recovers float(S) for two scores (replaces two v_cvt_f32_i32)
+//   FL_PREFETCH Q@K^T of tile t+1 issued before the softmax of tile t (QPW == 1)
+//   FL_LB2      register budget of 2 waves per SIMD (256 VGPRs) instead of 4 (128)
+//   FL_JIT / FL_LB4 (pipe kernel) operands read right before their MFMA / 4-wave register budget
+//   FL_EARLY    (pipe kernel) a tile's serial head (row max .. 1/sP) computed in the previous
+//               iteration beside its O update
+//   FL_KFOLD    (pipe kernel, with FL_MAGIC) the exponent read straight off the biased
+//               accumulator: the bias folded into the shift (see the kernel)
+// ABL (ablation builds only, results wrong): 1 no exp, 2 no P@V MFMA, 4 no Q@K^T MFMA,
+//   16 no compute (staging + barriers only), 64 no staging/barriers (recompute LDS buffer 0).
+// ---------------------------------------------------------------------------------------
+//   FL_DUMP     (pipe kernel) also store what the kernel itself computed: the int32 S^T of every
+//               tile (bias removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump:
+//               the bit-exact check of the production Q@K^T path; never the production launch)
+enum { FL_MAGIC = 1, FL_PREFETCH = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_EARLY = 32, FL_KFOLD = 64,
+       FL_DUMP = 256, FL_PIN = 512,
+       FL_ABL_NOMFMA = 2048, FL_ABL_NOEXP = 4096, FL_ABL_NODMA = 8192,
+       FL_DMA_SPLIT = 16384, FL_RING4 = 32768, FL_ABL_NOMFMA2 = 131072, FL_ACC1 = 262144, FL_TSHADOW = 524288, FL_PT = 1048576,
+       FL_FAIR = 2097152 };
+
+template <int D, int WAVES, int QPW, int SG, int FL, int ABL>
+__global__ __launch_bounds__(WAVES * 64, ((FL & FL_LB2) || QPW > 1) ? 2 : 4) void qmha_fa_int8_kernel(
+    const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sK, const float* __restrict__ sV,
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
+    constexpr int KS = D / 32;                    // i8 MFMA k-steps (QK) and d-blocks (PV)
+    constexpr int KBYTES = SG * 32 * D;           // K int8 per stage
+    constexpr int VBYTES = SG * 32 * D * 2;       // V f16 per stage
+    constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    constexpr bool MAGIC = FL & FL_MAGIC;
+    static_assert(KCH % 64 == 0 && VCH % 64 == 0, "a stage is whole KiB LDS-DMA pieces");
+    static_assert((KCH / SG) % 64 == 0, "a KV group is whole KiB pieces (D >= 32)");
+    static_assert(!(FL & FL_PREFETCH) || QPW == 1, "prefetch pipeline is for one Q group per wave");
+    __shared__ __attribute__((aligned(16))) int8_t lds[2][KBYTES + VBYTES];
+
+    QMHA_ENABLE_AGPR_MFMA();
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, col = lane & 31;
+
+    // per Q group state
+    v4i qop[QPW][KS];
+    float cq[QPW];
+    v16f o[QPW][KS];
+    float m_run[QPW], l_run[QPW], anchor[QPW];
+#pragma unroll
+    for (int j = 0; j < QPW; ++j) {
+        const int qg = (qb * WAVES + wave) * QPW + j;
+        if (qg < G) {  // wave-uniform
+            const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
+            cq[j] = quant_q_operand<D>(qrow, half, qop[j]) * c_log2;
+        } else {  // padding group: computes on a zero Q, never stored
+#pragma unroll
+            for (int s = 0; s < KS; ++s) qop[j][s] = v4i{0, 0, 0, 0};
+            cq[j] = 0.0f;
+        }
+#pragma unroll
+        for (int m = 0; m < KS; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[j][m][r] = 0.0f;
+        m_run[j] = 0.0f;   // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
+        l_run[j] = 0.0f;   // anchored: l * 2^(anchor - m)
+        anchor[j] = 0.0f;  // o = O * 2^(m - anchor), anchor <= m
+    }
+    const bool any_active = (qb * WAVES + wave) * QPW < G;  // wave-uniform
+
+    const int8_t* kbase = Ki + (size_t)bh * N * D;
+    const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
+    const float* skb = sK + (size_t)bh * G;
+    const float* svb = sV + (size_t)bh * G;
+    const int nst = (G + SG - 1) / SG;
+
+    // K/V stage staging by LDS-DMA (global_load_lds_dwordx4): each wave-instruction writes one
+    // contiguous KiB of LDS; the XOR swizzle of the LDS image is applied to the per-lane
+    // SOURCE address instead (linear destination + swizzled source + swizzled read).
+    auto issue = [&](int buf, int st) {
+        const int ngr = min(SG, G - st * SG);
+        const int8_t* ksrc = kbase + (size_t)st * KBYTES;
+        const char* vsrc = vbase + (size_t)st * VBYTES;
+        int8_t* L = lds[buf];
+#pragma unroll
+        for (int jj = 0; jj < (KCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;  // KiB piece of the K stage
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG)) {
+                const int idx = inst * 64 + lane;  // LDS chunk this lane fills
+                const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
+                __builtin_amdgcn_global_load_lds((gptr_t)(ksrc + row * D + 16 * cc), (lptr_t)(L + inst * 1024), 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < (VCH / 64 + WAVES - 1) / WAVES; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG)) {
+                const int idx = inst * 64 + lane;
+                const int grp = idx / (4 * D), w = idx % (4 * D);
+                const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
+                __builtin_amdgcn_global_load_lds((gptr_t)(vsrc + grp * 64 * D + d * 64 + 16 * cv),
+                                                 (lptr_t)(L + KBYTES + inst * 1024), 16, 0, 0);
+            }
+        }
+    };
+
+    v16i magic_blk;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) magic_blk[r] = MAGIC ? 0x4B400000 : 0;
+    if constexpr (MAGIC) asm volatile("" : "+v"(magic_blk));  // resident, not rematerialised per tile
+
+    // S^T = K Q^T of tile gi of the stage in LDS, for every Q group of the wave
+    auto qk = [&](const int8_t* L, int gi, v16i (&s)[QPW]) {
+        const int krow = gi * 32 + col;
+#pragma unroll
+        for (int j = 0; j < QPW; ++j) s[j] = MAGIC ? magic_blk : v16i{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const v4i kop = *reinterpret_cast<const v4i*>(L + krow * D + 16 * ((2 * ks + half) ^ chunk_swz<D>(krow)));
+#pragma unroll
+            for (int j = 0; j < QPW; ++j) {
+                if constexpr (ABL & 4) {  // opaque result, no instruction
+                    asm volatile("" : "=v"(s[j]) : "v"(kop), "v"(qop[j][ks]));
+                } else {
+                    s[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(kop, qop[j][ks], s[j], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    // one tile for every Q group: online softmax (fa_tc_int8_b.cu:281-346), P quantisation
+    // (:359), P@V (:366-371)
+    auto tile = [&](const int8_t* L, int gi, int t, v16i (&s)[QPW]) {
+        const float skt = skb[t], svt = svb[t];
+        float p[QPW][16];
+        v8h pop[QPW][2];
+        float scale[QPW];
+#pragma unroll
+        for (int j = 0; j < QPW; ++j) {
+            const float c = cq[j] * skt;  // sQ*sK*log2(e)/sqrt(d) >= 0
+            const int mxi = half_swap_max_i(tree_max16_i(s[j]));
+            const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
+            const float m_new = fmaxf(m_run[j], mx * c);
+            // tile max of p = exp(row max - m), then the max over the 32 query rows (:359)
+            const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(fmaf(mx, c, -m_new)));
+            const float sp = fmaxf(div127_fast(pmax), 1e-8f);  // sP = max(absmax/127, 1e-8)
+            const float invp = rcp_fast(sp);                   // 1/sP
+            // scores -> p = exp2(S*c - m).  Scalar fp32 ops throughout: on gfx950 v_pk_*_f32 issue
+            // at half the rate of v_fma/v_add (no throughput gain) and never overlap the MFMAs.
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float sv = MAGIC ? __int_as_float(s[j][r]) - QMHA_MAGIC_RNE : (float)s[j][r];
+                const float x = fmaf(sv, c, -m_new);
+                p[j][r] = (ABL & 1) ? x : __builtin_amdgcn_exp2f(x);
+            }
+            // Pi = rint(p/sP) as exact f16 integers (0..127)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                const float q0 = fmaf(p[j][r], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+                const float q1 = fmaf(p[j][r + 1], invp, QMHA_MAGIC_RNE) - QMHA_MAGIC_RNE;
+                const v2h h2 = __builtin_convertvector((v2f{q0, q1}), v2h);
+                pop[j][r >> 3][r & 7] = h2[0];
+                pop[j][r >> 3][(r & 7) + 1] = h2[1];
+            }
+            // row sum of the unquantised p (:336) + the other lane half
+            const float rs = half_swap_add(tree_sum16(p[j]));
+            // Anchored running state: o = O * 2^(m - anchor), l_run = l * 2^(m - anchor).  The
+            // reference's O = alpha*O + T*sP*sV and l = alpha*l + rowsum (:336,:344,:369-371)
+            // become o += T*sP*sV*2^(m_t - anchor) and l_run += rowsum*2^(m_t - anchor):
+            // mathematically identical, no per-tile pass over O and no alpha.
+            // re-anchor before the shift is formed, so 2^(m_new - anchor) <= 2^48 whatever the jump
+            // of the running max (a first tile ~100 log2 units above m0 = 0 would overflow it)
+            if (__builtin_amdgcn_ballot_w64(m_new - anchor[j] > 48.0f)) {
+                const float f = __builtin_amdgcn_exp2f(anchor[j] - m_new);
+#pragma unroll
+                for (int m = 0; m < KS; ++m)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[j][m][r] *= f;
+                l_run[j] *= f;
+                anchor[j] = m_new;
+            }
+            const float e = __builtin_amdgcn_exp2f(m_new - anchor[j]);
+            l_run[j] = fmaf(rs, e, l_run[j]);
+            m_run[j] = m_new;
+            scale[j] = sp * svt * e;
+        }
+#pragma unroll
+        for (int m = 0; m < KS; ++m) {
+            const int d = 32 * m + col;
+            const int8_t* vr = L + KBYTES + gi * 64 * D + d * 64;
+            v16f acc[QPW];
+#pragma unroll
+            for (int j = 0; j < QPW; ++j) acc[j] = v16f{};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const v8h vop = *reinterpret_cast<const v8h*>(vr + 16 * ((2 * ks + half) ^ chunk_swz<64>(d)));
+#pragma unroll
+                for (int j = 0; j < QPW; ++j) {
+                    if constexpr (ABL & 2) {  // opaque result, no instruction
+                        asm volatile("" : "=v"(acc[j]) : "v"(vop), "v"(pop[j][ks]));
+                    } else {
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop, pop[j][ks], acc[j], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < QPW; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[j][m][r] = fmaf(acc[j][r], scale[j], o[j][m][r]);
+        }
+    };
+
+    issue(0, 0);
+    qmha_dma_barrier();  // waits vmcnt(0): stage 0 has landed
+
+    for (int st = 0; st < nst; ++st) {
+        const int buf = (ABL & 64) ? 0 : (st & 1);
+        if (!(ABL & 64) && st + 1 < nst) issue(buf ^ 1, st + 1);  // buf^1 was released by the previous barrier
+        if (any_active && !(ABL & 16)) {
+            const int g0 = st * SG;
+            const int ngr = min(SG, G - g0);  // wave-uniform
+            const int8_t* L = lds[buf];
+            if ((FL & FL_PREFETCH) && ngr == SG) {
+                // straight-line stage: Q@K^T of tile gi+1 is issued before tile gi's softmax
+                v16i s_cur[QPW], s_nxt[QPW];
+                qk(L, 0, s_cur);
+#pragma unroll
+                for (int gi = 0; gi < SG; ++gi) {
+                    if (gi + 1 < SG) qk(L, gi + 1, s_nxt);
+                    // pin the pipeline depth to one tile (the scheduler would hoist every
+                    // Q@K^T of the stage and the live S tiles cost registers)
+                    __builtin_amdgcn_sched_barrier(0);
+                    QMHA_ISA_MARK();
+                    tile(L, gi, g0 + gi, s_cur);
+                    QMHA_ISA_MARK();
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < QPW; ++j) s_cur[j] = s_nxt[j];
+                }
+            } else if (ngr == SG) {
+#pragma unroll
+                for (int gi = 0; gi < SG; ++gi) {
+                    v16i s[QPW];
+                    qk(L, gi, s);
+                    QMHA_ISA_MARK();
+                    tile(L, gi, g0 + gi, s);
+                    QMHA_ISA_MARK();
+                }
+            } else {
+                for (int gi = 0; gi < ngr; ++gi) {
+                    v16i s[QPW];
+                    qk(L, gi, s);
+                    tile(L, gi, g0 + gi, s);
+                }
+            }
+        }
+        if constexpr (!(ABL & 64)) qmha_dma_barrier();  // vmcnt(0) + barrier: stage st+1 landed, stage st released
+    }
+
+    // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20 -----------------
+#pragma unroll
+    for (int j = 0; j < QPW; ++j) {
+        const int qg = (qb * WAVES + wave) * QPW + j;
+        if (qg >= G) continue;  // wave-uniform
+        const float unanchor = __builtin_amdgcn_exp2f(anchor[j] - m_run[j]);  // 2^(anchor - m)
+        const float l = l_run[j] * unanchor;
+        const bool ok = l > 1e-20f;
+        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
+#pragma unroll
+        for (int m = 0; m < KS; ++m)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                v4f w;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) w[jj] = ok ? (o[j][m][4 * g4 + jj] * unanchor) / l : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Software-pipelined main kernel (one Q group per wave).
+//
+// Iteration t runs the softmax of tile t on the VALU while the matrix core executes
+// P@V of tile t-1 and Q@K^T of tile t+1 -- all three independent -- so each wave covers its
+// own MFMA time with its own VALU work instead of relying on co-resident waves.  The order
+// inside an iteration is pinned with sched_barrier fences (chunks of softmax VALU between
+// single MFMAs); every chained MFMA pair is split by VALU work.
+// K/V: stages of 2 KV groups, a 3-deep LDS ring filled by LDS-DMA two tiles ahead; one
+// barrier per stage, before its odd tile (the DMA of stage s+2 is issued right after it).
+// ---------------------------------------------------------------------------------------
+#ifndef QMHA_PT_D128_SCHED
+#define QMHA_PT_D128_SCHED 0
+#endif
+// fa_tc_int8_pt's MFMA placement: the j-th (j < 2) MFMA issued after VALU region s (s < 6) of an
+// iteration, -1 for none; op 2m + ks = P@V of d-block m, k-step ks (tile t-1), op 8 + ks = Q@K^T
+// k-step ks (tile t+1).  P@V(m, 1) trails P@V(m, 0) by >= 2 slots; Q@K^T sits mid-iteration so
+// the next tile's scores land before its head.
+__host__ __device__ constexpr int pt_slot_op(int D, int s, int j) {
+    constexpr int d32[6][2] = {{0, -1}, {-1, -1}, {1, -1}, {8, -1}, {-1, -1}, {-1, -1}};
+    constexpr int d64[6][2] = {{0, -1}, {2, -1}, {1, -1}, {8, -1}, {9, -1}, {3, -1}};
+    constexpr int d128[6][2] = {{0, 2}, {4, 6}, {1, 3}, {8, 9}, {10, 11}, {5, 7}};
+    // A/B (QMHA_PT_D128_SCHED=1): every Q@K^T step in its own slot, beside a P@V
+    constexpr int d128b[6][2] = {{0, 8}, {2, 9}, {4, 10}, {6, 11}, {1, 3}, {5, 7}};
+    return D == 32 ? d32[s][j] : D == 64 ? d64[s][j] : (QMHA_PT_D128_SCHED ? d128b[s][j] : d128[s][j]);
+}
+
+template <int N>
+__device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
+}
+
+#ifdef QMHA_TIMELINE  // profiling builds only: per-workgroup start / end wall clock of the last launch
+__device__ unsigned long long qmha_tl_buf[4][1 << 17];
+__device__ __forceinline__ unsigned long long qmha_tl_now() { return wall_clock64(); }
+extern "C" int qmha_debug_timeline(unsigned long long* host) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(host, HIP_SYMBOL(qmha_tl_buf), sizeof(qmha_tl_buf));
+    return (int)e;
+}
+#endif
+#ifndef QMHA_PIPE_ATTR  // profiling builds may cap the register budget, e.g. amdgpu_num_vgpr
+#define QMHA_PIPE_ATTR
+#endif
+template <int D, int WAVES, int FL, int PAD = 0>
+__global__ QMHA_PIPE_ATTR __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
+    const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sK, const float* __restrict__ sV,
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
+    const float* __restrict__ sQt = nullptr) {
+    // FL_RING4 (d = 64): a 4-slot ring filled three stages ahead; the stage barrier waits with a
+    // counted vmcnt (the newest stage's pieces stay in flight across it) instead of vmcnt(0)
+    constexpr bool RING4 = FL & FL_RING4;
+    static_assert(!RING4 || D == 64, "FL_RING4: the counted wait assumes 3 pieces per wave and stage (d = 64)");
+    constexpr int SG = 2, RING = RING4 ? 4 : 3, PF = RING - 1;  // PF: stages in flight ahead
+    constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
+    constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
+    constexpr int SBYTES = KBYTES + VBYTES;
+    constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    constexpr bool MAGIC = FL & FL_MAGIC;
+    __shared__ __attribute__((aligned(16))) int8_t lds[RING][SBYTES];
+
+    QMHA_ENABLE_AGPR_MFMA();
+#ifdef QMHA_TIMELINE
+    const unsigned long long tl_t0 = qmha_tl_now();
+#endif
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, col = lane & 31;
+    const int qg = qb * WAVES + wave;
+    const bool active = qg < G;  // wave-uniform; an inactive wave still stages and syncs
+
+    v4i qop[D / 32];
+    float cq = 0.0f;
+    constexpr bool DUMP = FL & FL_DUMP;
+    // FL_PT (fa_tc_int8_pt, per-tensor mode): sQt / sK / sV hold one scale per head slice, P is
+    // quantised with the static scale 1/127, so every tile's P@V is in the same unit and
+    // accumulates straight into O (the MFMA C operand); O is rescaled by alpha when a row's
+    // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
+    constexpr bool PT = FL & FL_PT;
+    constexpr bool FAIR = FL & FL_FAIR;
+    static_assert(!PT || !(FL & (FL_TSHADOW | FL_ACC1 | FL_ABL_NOMFMA | FL_ABL_NOMFMA2)), "FL_PT combinations");
+    if (active) {
+        const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
+        const float sq = quant_q_operand<D>(qrow, half, qop, PT ? sQt[bh] : 0.0f);
+        cq = sq * c_log2;
+        if constexpr (DUMP) {  // the Q operand as held in registers: lane (col, half), k-step s
+            int8_t* qd = dbg.Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * D + 16 * half;
+#pragma unroll
+            for (int s = 0; s < D / 32; ++s) *reinterpret_cast<v4i*>(qd + 32 * s) = qop[s];
+            if (lane == 0) dbg.sQ[(size_t)bh * G + qg] = sq;
+        }
+    } else {
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) qop[ks] = v4i{0, 0, 0, 0};
+    }
+    const int8_t* kbase = Ki + (size_t)bh * N * D;
+    const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
+    const float* skb = sK + (size_t)bh * (PT ? 1 : G);  // PT: one scale per head slice
+    const float* svb = sV + (size_t)bh * (PT ? 1 : G);
+    const int nst = (G + SG - 1) / SG;
+
+    // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
+    // stage offset rides in soffset, so a stage costs no address arithmetic on the VALU
+    constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
+    int koff[KJ], voff[VJ];
+#pragma unroll
+    for (int jj = 0; jj < KJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int row = idx / (D / 16), cc = (idx % (D / 16)) ^ chunk_swz<D>(row);
+        koff[jj] = row * D + 16 * cc;
+    }
+#pragma unroll
+    for (int jj = 0; jj < VJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int grp = idx / (4 * D), w = idx % (4 * D);
+        const int d = w >> 2, cv = (w & 3) ^ chunk_swz<64>(d);
+        voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
+    }
+    // stage st into ring slot `slot` (= st % RING; a compile-time constant in the unrolled loop)
+    // piece `pc` (< KJ + VJ: this wave's K pieces, then its V pieces) of stage st into ring slot
+    // `slot`; pieces < 0 = all of them
+    auto issue_piece = [&](int st, int slot, int pc) {
+        if constexpr (FL & FL_ABL_NODMA) return;  // timing perturbation: stages never refilled
+        const int ngr = min(SG, G - st * SG);
+        int8_t* L = lds[slot];
+#pragma unroll
+        for (int jj = 0; jj < KJ; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if ((pc < 0 || pc == jj) && inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
+                buffer_load_lds16(kbase, N * D, (lptr_t)(L + inst * 1024), koff[jj], st * KBYTES);
+        }
+#pragma unroll
+        for (int jj = 0; jj < VJ; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if ((pc < 0 || pc == KJ + jj) && inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
+                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
+        }
+    };
+    auto issue_at = [&](int st, int slot) { issue_piece(st, slot, -1); };
+    auto issue = [&](int st) { issue_at(st, st % RING); };
+    // operand reads of the tile in ring slot `slot`, position `par` (0/1) of its stage
+    auto kop_at = [&](int slot, int par, int ks) {
+        const int8_t* L = lds[slot];
+        const int krow = par * 32 + col;
+        return *reinterpret_cast<const v4i*>(L + krow * D + 16 * ((2 * ks + half) ^ chunk_swz<D>(krow)));
+    };
+    auto vop_at = [&](int slot, int par, int m, int ks) {
+        const int8_t* L = lds[slot];
+        const int d = 32 * m + col;
+        return *reinterpret_cast<const v8h*>(L + KBYTES + par * 64 * D + d * 64 +
+                                             16 * ((2 * ks + half) ^ chunk_swz<64>(d)));
+    };
+    auto kop_of = [&](int t, int ks) { return kop_at((t >> 1) % RING, t & 1, ks); };
+    auto vop_of = [&](int t, int m, int ks) { return vop_at((t >> 1) % RING, t & 1, m, ks); };
+
+    v16i magic_blk;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) magic_blk[r] = MAGIC ? 0x4B400000 : 0;
+    if constexpr (MAGIC) asm volatile("" : "+v"(magic_blk));
+
+    // ---- MFMA schedule of one iteration, per head size.  An iteration issues the P@V MFMAs of
+    // tile t-1 (PV(m, ks): d-block m < MB, 16-key half ks) and the Q@K^T chain of tile t+1
+    // (QK(ks), ks < KS) between the six VALU chunks A..F of tile t's softmax; kSlot[c] MFMAs
+    // follow chunk c, in kOps order.  Every chained pair (same accumulator) is split by VALU.
+    constexpr int MB = D / 32;  // 32-wide d-blocks of O^T (PV accumulators)
+    constexpr int KS = D / 32;  // 32-deep k-steps of the i8 Q@K^T
+    constexpr int NOPS = 2 * MB + KS;
+    auto PVop = [](int m, int ks) { return 2 * m + ks; };
+    auto QKop = [](int ks) { return 1000 + ks; };
+    (void)PVop;
+    (void)QKop;
+    constexpr int kSlot64[6] = {1, 1, 1, 1, 1, 1};
+    constexpr int kOps64[6] = {0, 2, 1, 1000, 3, 1001};  // PV00 PV10 PV01 QK0 PV11 QK1
+    // FL_ACC1 (d = 64): ONE 16-register P@V accumulator for both d-blocks: PV00 PV01, block 0 folded
+    // into O in chunk D, PV10 PV11, block 1 folded at the iteration's end (16 VGPRs fewer)
+    constexpr bool ACC1 = (FL & FL_ACC1) && D == 64;
+    constexpr int kOps64a[6] = {0, 1, 1000, 2, 1001, 3};  // PV00 PV01 QK0 PV10 QK1 PV11
+    constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
+    constexpr int kOps32[3] = {0, 1, 1000};  // PV00 PV01 QK0
+    constexpr int kSlot128[6] = {2, 2, 2, 2, 2, 2};
+#ifndef QMHA_D128_SCHED
+#define QMHA_D128_SCHED 1
+#endif
+    // d = 128 (QMHA_D128_SCHED 1): A PV00 PV10 | B PV20 QK0 | C PV30 PV01 | D QK1 PV11 | E PV21 QK2 |
+    // F PV31 QK3 -- every chained pair (PV(m,0) -> PV(m,1), QK(k) -> QK(k+1)) is separated by a VALU
+    // chunk and another MFMA (round-2 ADVICE: the r02 table, QMHA_D128_SCHED 0, issued QK0 -> QK1 and
+    // QK2 -> QK3 back to back)
+    constexpr int kOps128[12] = {0, 2, 4, QMHA_D128_SCHED ? 1000 : 6, QMHA_D128_SCHED ? 6 : 1000,
+                                 QMHA_D128_SCHED ? 1 : 1001, QMHA_D128_SCHED ? 1001 : 1, 3, 5,
+                                 QMHA_D128_SCHED ? 1002 : 7, QMHA_D128_SCHED ? 7 : 1002, 1003};
+    auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
+    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? (ACC1 ? kOps64a[i] : kOps64[i]) : kOps128[i]); };
+    static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
+    static_assert(NOPS == (D == 32 ? 3 : (D == 64 ? 6 : 12)), "MFMA schedule table");
+
+    v16f o[MB];                  // O^T, d-block m (anchored)
+#pragma unroll
+    for (int m = 0; m < MB; ++m) o[m] = v16f{};
+    float m_run = 0.0f;          // m0 = 0 (fa_tc_int8_b.cu:402), log2 units
+    float l_run = 0.0f;          // l * 2^(anchor - m) over this lane's half of the keys
+    float anchor = 0.0f;
+    v16i s_cur, s_nxt;           // S^T of tiles t and t+1
+    // FL_ABL_NOMFMA / FL_ABL_NOEXP / FL_ABL_NODMA (timing perturbations, A/B builds only; results
+    // are wrong): every MFMA / every exp of the softmax replaced by an empty asm that keeps its
+    // operands and result live, so the rest of the loop compiles to the same VALU work / no
+    // LDS-DMA issued (barriers and operand reads unchanged)
+    constexpr bool NOMFMA = FL & FL_ABL_NOMFMA, NOEXP = FL & FL_ABL_NOEXP;
+    // FL_ABL_NOMFMA2 (r03): the same without a single added instruction -- the Q@K^T "result"
+    // keeps the prologue's bias-only block (S = 0: sane scores, no re-anchoring), each P@V
+    // "result" is a fresh undefined register block (ks = 0) or the previous one (ks = 1), so the
+    // compiled VALU / LDS / DMA stream equals the real kernel's minus the MFMAs
+    constexpr bool NOMFMA2 = FL & FL_ABL_NOMFMA2;
+    if constexpr (NOMFMA2) s_nxt = magic_blk;
+    auto qk = [&](const v4i& kk, int ks) {
+        if constexpr (NOMFMA2) {
+            asm volatile("" : "+v"(s_nxt) : "v"(kk), "v"(qop[ks]));
+        } else if constexpr (NOMFMA) {
+            if (ks == 0) s_nxt = magic_blk;
+            asm volatile("" : "+v"(s_nxt) : "v"(kk), "v"(qop[ks]));
+        } else {
+            s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
+        }
+    };
+    v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
+    float scale_prev = 0.0f;
+    v16f a[MB];                  // P@V accumulators of the pending tile
+    constexpr bool EARLY = FL & FL_EARLY;
+    constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
+    // FL_KFOLD (with FL_MAGIC): the exponent of key j is fma(A_j, c', -Kn) straight from the
+    // biased accumulator A_j = 1.5*2^23 + S_j (as a float), with Kn = 1.5*2^23*c' + m.  c' is the
+    // score scale rounded to 22 significant bits, so 1.5*2^23*c' is exact and the shift the
+    // exponents actually get, m_eff = Kn - 1.5*2^23*c', is exact too (Sterbenz: |m| < 2^20 c').
+    // So p'_j = 2^(s_j - m_eff) = p_j * 2^(m_eff - m) with |m_eff - m| <= ulp(Kn)/2 (~1e-4): the
+    // per-row factor f = 2^(m_eff - m) (= 1 + (m_eff - m) ln 2 to < 1 ulp) is folded into the
+    // row's 1/sP and its row-sum scale, because the P tile's one scale sP is shared by rows with
+    // different f.  Saves the 16 bias subtractions per tile for 4 per-row operations.
+    constexpr bool KFOLD = MAGIC && (FL & FL_KFOLD);
+    // FL_PIN: each softmax chunk's results pass through an empty volatile asm at the chunk's end,
+    // so IR-level code motion cannot sink the chunk past the sched_barrier fences (without it the
+    // P quantisation sinks into the next iteration and whole chunks cross the stage barrier,
+    // leaving runs of back-to-back MFMAs with no VALU between them)
+    constexpr bool PIN = FL & FL_PIN;
+    // FL_EARLY: the serial head of a tile (row max -> running max -> P-tile max -> sP -> 1/sP)
+    // runs at the end of the previous iteration, in one scheduling region with that
+    // iteration's O update, so its latency chain interleaves with independent work
+    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f;
+    // PT: the score scale sQ * sK * log2(e) / sqrt(d) is one constant per head (KFOLD-rounded once)
+    const float c_pt = PT ? (KFOLD ? __int_as_float((__float_as_int(cq * skb[0]) + 2) & ~3) : cq * skb[0]) : 0.0f;
+    auto head = [&](const v16i& s, int t) {
+        float c = PT ? c_pt : cq * skb[t];
+        const int mxi = half_swap_max_i(tree_max16_i(s));
+        float xmax;
+        if constexpr (KFOLD) {
+            if constexpr (!PT) c = __int_as_float((__float_as_int(c) + 2) & ~3);
+            const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;  // exact float(S_max)
+            h_m = fmaxf(m_run, sfmax * c);
+            h_k = fmaf(c, QMHA_MAGIC_RNE, h_m);
+            const float delta = fmaf(c, -QMHA_MAGIC_RNE, h_k) - h_m;  // m_eff - m, exact
+            h_f = fmaf(delta, 0.69314718055994531f, 1.0f);
+            xmax = fmaf(sfmax, c, -h_m);
+        } else {
+            const float mx = MAGIC ? __int_as_float(mxi) - QMHA_MAGIC_RNE : (float)mxi;
+            h_m = fmaxf(m_run, mx * c);
+            xmax = fmaf(mx, c, -h_m);
+        }
+        h_c = c;
+        if constexpr (PT) {  // alpha = 2^(m - m_new); Pi = rint(p * 127) (static P scale), f folded in
+            (void)xmax;
+            h_alpha = __builtin_amdgcn_exp2f(m_run - h_m);
+            h_invp = KFOLD ? 127.0f * h_f : 127.0f;
+            return;
+        }
+        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
+        // sP = max(pmax / 127, 1e-8) as pm / 127 with pm = max(pmax, 127e-8), and 1/sP by one
+        // v_rcp: within ~2 ulp of the reference's rounded 1/sP, which moves a Pi only when p/sP
+        // lies that close to a .5 boundary (the same class as exp2 vs expf).  h_sp carries the
+        // 2^24 of the f16-subnormal P entries (Pi * 2^-24)
+        const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
+        h_invp = __builtin_amdgcn_rcpf(sp);
+        if constexpr (KFOLD) h_invp *= h_f;
+        h_sp = sp * 16777216.0f;
+    };
+
+    issue(0);
+    if (nst > 1) issue(1);
+    if (RING4 && nst > 2) issue(2);
+    qmha_dma_barrier();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qk(kop_of(0, ks), ks);
+    s_cur = s_nxt;
+    if constexpr (EARLY) head(s_cur, 0);
+
+#define QMHA_FENCE() __builtin_amdgcn_sched_barrier(0)
+    // one pipeline iteration; HP / HN (compile time): a tile t-1 to finish / a tile t+1 to start.
+    // PH (compile time): -1, or u with t = 6j + 1 + u, which fixes every ring slot and stage
+    // position this iteration touches (the ring has 3 slots of 2 tiles: period 6), so operand
+    // reads are LDS immediates and the per-tile slot arithmetic disappears
+    auto iter = [&](int t, auto HP, auto HN, auto PH) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
+        // FL_DMA_SPLIT: the stage's LDS-DMA pieces issue one after each of the first MFMAs of the
+        // iteration (in the MFMA's shadow) instead of together right after the barrier
+        constexpr bool SPLIT = FL & FL_DMA_SPLIT;
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        const bool dma_now = odd && dma_st < nst;  // uniform
+        auto dma_piece = [&](int pc) {
+            if constexpr (SPLIT)
+                if (dma_now && pc < KJ + VJ) issue_piece(dma_st, dma_slot, pc);
+        };
+        if (odd) {  // uniform
+            if constexpr (RING4) {
+                // stage (t+1)/2 must have landed; stage (t+1)/2 + 1 (this wave's 3 pieces, issued
+                // last) may stay in flight unless it is the (possibly partial) last stage
+                const int s1 = (t + 1) / 2 + 1;
+                if (s1 < nst - 1 || (s1 == nst - 1 && G % SG == 0))
+                    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // raw barrier: __syncthreads' workgroup fence would add a vmcnt(0) of its own
+                __builtin_amdgcn_s_barrier();
+            } else {
+                qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            }
+            if (!SPLIT && dma_now) issue_at(dma_st, dma_slot);
+        }
+        if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (32x32 accumulator map)
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    sd[8 * (r >> 2) + 4 * half + (r & 3)] = MAGIC ? s_cur[r] - 0x4B400000 : s_cur[r];
+            }
+        }
+        // operand reads for this iteration's MFMAs (JIT: right before each MFMA instead)
+        v8h vv[MB][2];
+        v4i kk[KS];
+        if constexpr (has_prev && !JIT) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
+        }
+        if constexpr (has_next && !JIT) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) kk[ks] = kop(ks);
+        }
+        QMHA_FENCE();
+        // the MFMAs that follow VALU chunk c (compile-time after unrolling)
+        int op_i = 0;
+        auto mfmas = [&](int c) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j < slot_n(c)) {
+                    const int op = op_at(op_i++);
+                    if (op >= 1000) {
+                        const int ks = op - 1000;
+                        if (has_next) qk(JIT ? kop(ks) : kk[ks], ks);
+                    } else {
+                        const int m = op >> 1, ks = op & 1;
+                        if (has_prev) {
+                            if constexpr (NOMFMA2) {
+                                if (ks == 0)
+                                    asm volatile("" : "=v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                                else
+                                    asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                            } else if constexpr (NOMFMA) {
+                                if (ks == 0) a[m] = v16f{};
+                                asm volatile("" : "+v"(a[m]) : "v"(JIT ? vop(m, ks) : vv[m][ks]), "v"(pp[ks]));
+                            } else {
+                                if constexpr (PT) {  // P@V straight into O
+                                    o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                                  o[m], 0, 0, 0);
+                                } else {
+                                    v16f& acc = ACC1 ? a[0] : a[m];
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                                 ks == 0 ? v16f{} : acc, 0, 0, 0);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        // ---- A: row max, running max, P-tile max (fa_tc_int8_b.cu:286-303, :359)
+        if constexpr (!EARLY) {
+            head(s_cur, t);
+            QMHA_FENCE();
+        }
+        const float c = h_c, m_new = h_m, kn = h_k;
+        // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
+        // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
+        // overflow it); the pending tile t-1 carries its factor in scale_prev
+        if (!PT && __builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+            const float f = __builtin_amdgcn_exp2f(anchor - m_new);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= f;
+            l_run *= f;
+            scale_prev *= f;
+            anchor = m_new;
+        }
+        mfmas(0);
+        dma_piece(0);
+        QMHA_FENCE();
+        // ---- B: P scale, scores of rows 0..7
+        const float sp = h_sp, invp = h_invp;
+        const float e = PT ? 1.0f : __builtin_amdgcn_exp2f(m_new - anchor);
+        float x[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            if constexpr (KFOLD) {
+                x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+            } else {
+                const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+                x[r] = fmaf(sv, c, -m_new);
+            }
+        }
+        if constexpr (PIN) pin_regs(x, 0, 8);
+        QMHA_FENCE();
+        mfmas(1);
+        dma_piece(1);
+        QMHA_FENCE();
+        // ---- C: scores of rows 8..15
+#pragma unroll
+        for (int r = 8; r < 16; ++r) {
+            if constexpr (KFOLD) {
+                x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+            } else {
+                const float sv = MAGIC ? __int_as_float(s_cur[r]) - QMHA_MAGIC_RNE : (float)s_cur[r];
+                x[r] = fmaf(sv, c, -m_new);
+            }
+        }
+        if constexpr (PIN) pin_regs(x, 8, 16);
+        QMHA_FENCE();
+        mfmas(2);
+        dma_piece(2);
+        QMHA_FENCE();
+        // ---- D: p = exp2, rows 0..7
+        float p[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            if constexpr (NOEXP) {
+                p[r] = x[r];
+                asm volatile("" : "+v"(p[r]));
+            } else {
+                p[r] = __builtin_amdgcn_exp2f(x[r]);
+            }
+        }
+        if constexpr (PIN) pin_regs(p, 0, 8);
+        if constexpr (ACC1 && has_prev) {  // block 0 of the pending tile (PV00, PV01 issued after A, B)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[0][r] = fmaf(a[0][r], scale_prev, o[0][r]);
+        }
+        QMHA_FENCE();
+        mfmas(3);
+        QMHA_FENCE();
+        // ---- E: p = exp2, rows 8..15
+#pragma unroll
+        for (int r = 8; r < 16; ++r) {
+            if constexpr (NOEXP) {
+                p[r] = x[r];
+                asm volatile("" : "+v"(p[r]));
+            } else {
+                p[r] = __builtin_amdgcn_exp2f(x[r]);
+            }
+        }
+        if constexpr (PIN) pin_regs(p, 8, 16);
+        QMHA_FENCE();
+        mfmas(4);
+        QMHA_FENCE();
+        // ---- F: Pi = rint(p/sP) (:317-321), carried as the f16 subnormal Pi * 2^-24:
+        // fma(p, 1/sP, 1.5 * 2^23) rounds half-even to an integer whose float bits end in Pi,
+        // and those low 16 bits are exactly the f16 encoding of Pi * 2^-24; one byte permute
+        // packs two entries.  P@V then yields T * 2^-24 exactly (T < 2^20); the O scale
+        // carries the 2^24 back.
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
+            const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
+            pc[r >> 2][2 * (r & 3)] = h2[0];
+            pc[r >> 2][2 * (r & 3) + 1] = h2[1];
+        }
+        if constexpr (PIN) {
+            asm volatile("" : "+v"(pc[0]));
+            asm volatile("" : "+v"(pc[1]));
+        }
+        QMHA_FENCE();
+        mfmas(5);
+        QMHA_FENCE();
+        // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
+        // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
+        const float rs = tree_sum16(p);
+        if constexpr (PT)
+            l_run = fmaf(h_alpha, l_run, KFOLD ? rs * h_f : rs);  // l = alpha * l + sum(p)
+        else
+            l_run = fmaf(rs, KFOLD ? e * h_f : e, l_run);
+        m_run = m_new;
+        const float scale_t = PT ? 0.0f : sp * svb[t] * e;  // sp carries 2^24: P entries are Pi * 2^-24
+        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor)); PT: O already
+        // holds tile t-1's P@V, and takes this tile's alpha before tile t's P@V lands next iteration
+        if constexpr (PT) {
+            if (__builtin_amdgcn_ballot_w64(h_alpha != 1.0f)) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m) o[m] *= h_alpha;
+            }
+        } else if constexpr (has_prev) {
+#pragma unroll
+            for (int m = ACC1 ? 1 : 0; m < MB; ++m)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[ACC1 ? 0 : m][r], scale_prev, o[m][r]);
+        }
+        if constexpr (EARLY && has_next) head(s_nxt, t + 1);  // same region as the O update
+        QMHA_FENCE();
+        // rotate the pipeline
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        scale_prev = scale_t;
+        if constexpr (has_next) s_cur = s_nxt;
+    };
+    // ---- FL_TSHADOW (d = 64): the same work, re-spaced around the MFMAs by instruction class.  On
+    // gfx950 an executing MFMA blocks the SIMD's full-rate fp32 VALU (v_fma/v_add/v_mul: no overlap)
+    // but not its transcendental and quarter-rate ops (v_exp, v_rcp, v_perm, v_max3, DPP, permlane):
+    // ~25 cycles of those hide per 32-cycle MFMA at 1-4 waves/SIMD (tools/ubench/mfma_fill.hip ->
+    // profiles/r03/ubench_mfma_fill.txt).  So every MFMA is followed by a group of such ops (the
+    // tile head after QK1 / PV11, four exps after each P@V / Q@K^T MFMA, the perms) and only then
+    // by the full-rate work (scores, quantisation, row sum, O folds), each group in its own
+    // sched_barrier region so the compiler keeps the order.
+    // MFMAs: m0 PV00, m1 PV10, m2 PV01, m3 QK0, m4 QK1, m5 PV11.  The O fold of d-block 0 of tile
+    // t-1 runs in this iteration (after m2), that of d-block 1 in the next one (after its head;
+    // scale_pp keeps tile t-1's scale for it)
+    constexpr bool TSHADOW = (FL & FL_TSHADOW) && D == 64;
+    static_assert(!(FL & FL_TSHADOW) || (D == 64 && KFOLD && !JIT && !ACC1 && !EARLY && !RING4 && !(FL & FL_DMA_SPLIT) &&
+                                         !NOMFMA && !NOMFMA2 && !NOEXP && !PIN),
+                  "FL_TSHADOW: d = 64 MAGIC|KFOLD schedule (no ablation / JIT / ring variants)");
+    float scale_pp = 0.0f;  // tile t-2's O scale for its d-block-1 fold (a[1] starts at 0: a no-op fold)
+    if constexpr (TSHADOW) a[1] = v16f{};
+    auto iter_ts = [&](int t, auto HP, auto HN, auto PH) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        if (odd) {  // uniform
+            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            if (dma_st < nst) issue_at(dma_st, dma_slot);
+        }
+        if constexpr (DUMP) {
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sd[8 * (r >> 2) + 4 * half + (r & 3)] = s_cur[r] - 0x4B400000;
+            }
+        }
+        // MFMA operands are read from LDS one region ahead of their MFMA (short live ranges)
+        v8h vv[MB][2];
+        v4i kk[KS];
+        auto rd_v = [&](int m, int ks) {
+            if constexpr (has_prev) vv[m][ks] = vop(m, ks);
+        };
+        auto rd_k = [&](int ks) {
+            if constexpr (has_next) kk[ks] = kop(ks);
+        };
+        auto pv = [&](int m, int ks) {
+            if constexpr (has_prev)
+                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][ks], pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+        };
+        auto qkm = [&](int ks) {
+            if constexpr (has_next) qk(kk[ks], ks);
+        };
+        rd_v(0, 0);
+        rd_v(1, 0);
+        float x[16], p[16], q[16];
+        auto exps = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        };
+        auto quant = [&](int r0, int r1) {  // Pi = rint(p/sP) in the low bits (f16 subnormal Pi * 2^-24)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
+        };
+        auto perms = [&](int j0, int j1) {  // pair j = rows 2j, 2j+1
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j >= j0 && j < j1) {
+                    const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(q[2 * j + 1]),
+                                                                               __float_as_uint(q[2 * j]), 0x05040100u));
+                    pc[j >> 2][2 * (j & 3)] = h2[0];
+                    pc[j >> 2][2 * (j & 3) + 1] = h2[1];
+                }
+            // pin: IR-level sinking (which sched_barrier does not constrain) would otherwise move the
+            // packs to their use in the next iteration, away from this MFMA shadow
+            asm volatile("" : "+v"(pc[0]), "+v"(pc[1]));
+        };
+        QMHA_FENCE();
+        // ---- R0 (behind m4 / m5 of the previous iteration): the tile head (row max tree, permlanes,
+        // DPP P-tile max, exp, rcp: quarter-rate / transcendental), the rare re-anchor
+        head(s_cur, t);
+        const float c = h_c, m_new = h_m, kn = h_k;
+        if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+            const float f = __builtin_amdgcn_exp2f(anchor - m_new);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= f;
+            l_run *= f;
+            scale_prev *= f;
+            scale_pp *= f;
+            anchor = m_new;
+        }
+        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
+        QMHA_FENCE();
+        // full rate: d-block 1 of tile t-2 (PV11 issued last iteration), scores 0..7
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        QMHA_FENCE();
+        pv(0, 0);  // m0
+        QMHA_FENCE();
+        exps(0, 4);
+        QMHA_FENCE();
+        rd_v(0, 1);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        quant(0, 4);
+        float rs0 = (p[0] + p[1]) + (p[2] + p[3]);
+        asm volatile("" : "+v"(rs0));
+        QMHA_FENCE();
+        pv(1, 0);  // m1
+        QMHA_FENCE();
+        exps(4, 8);
+        perms(0, 2);
+        QMHA_FENCE();
+        rd_k(0);
+        quant(4, 8);
+        float rs1 = (p[4] + p[5]) + (p[6] + p[7]);
+        asm volatile("" : "+v"(rs1));
+        QMHA_FENCE();
+        pv(0, 1);  // m2
+        QMHA_FENCE();
+        exps(8, 12);
+        perms(2, 4);
+        QMHA_FENCE();
+        rd_k(1);
+        quant(8, 12);
+        float rs2 = (p[8] + p[9]) + (p[10] + p[11]);
+        asm volatile("" : "+v"(rs2));
+        QMHA_FENCE();
+        qkm(0);  // m3
+        QMHA_FENCE();
+        exps(12, 16);
+        perms(4, 6);
+        QMHA_FENCE();
+        // d-block 0 of tile t-1 (PV00 m0, PV01 m2)
+        if constexpr (has_prev) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[0][r] = fmaf(a[0][r], scale_prev, o[0][r]);
+        }
+        rd_v(1, 1);
+        quant(12, 16);
+        float rs3 = (p[12] + p[13]) + (p[14] + p[15]);
+        asm volatile("" : "+v"(rs3));
+        QMHA_FENCE();
+        qkm(1);  // m4
+        QMHA_FENCE();
+        perms(6, 8);
+        QMHA_FENCE();
+        l_run = fmaf((rs0 + rs1) + (rs2 + rs3), e * h_f, l_run);
+        m_run = m_new;
+        const float scale_t = h_sp * svb[t] * e;
+        QMHA_FENCE();
+        pv(1, 1);  // m5
+        QMHA_FENCE();
+        // rotate the pipeline
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        scale_pp = has_prev ? scale_prev : 0.0f;
+        scale_prev = scale_t;
+        if constexpr (has_next) s_cur = s_nxt;
+    };
+    // ---- FL_PT: the per-tensor iteration as explicit sched_barrier regions (the generic body above
+    // keeps its live ranges for the per-block fold and spills in this mode).  Six regions R0..R5 of
+    // VALU work; after region s the MFMAs of pt_slot_op(D, s, .) issue (transcendental /
+    // quarter-rate work first in each region, full-rate work after it); operands are read from LDS
+    // in the region before their slot's predecessor (two slots ahead).  P@V accumulates straight
+    // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
+    // P@V of t-2 has), so no MFMA result is waited on.
+    // iter_pt forms the exponent as fma(accumulator bits, c', -Kn): the MAGIC-biased accumulator and KFOLD
+    static_assert(!PT || (MAGIC && KFOLD), "FL_PT needs FL_MAGIC | FL_KFOLD");
+    float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
+    auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
+        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
+        constexpr int ph = decltype(PH)::value;
+        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
+        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
+        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
+        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
+        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
+        const int dma_st = (t >> 1) + PF;
+        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
+        if (odd) {  // uniform
+            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
+            if (dma_st < nst) issue_at(dma_st, dma_slot);
+        }
+        if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (32x32 accumulator map)
+            if (active) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sd[8 * (r >> 2) + 4 * half + (r & 3)] = s_cur[r] - 0x4B400000;
+            }
+        }
+        v8h vv[MB][2];
+        v4i kk[KS];
+        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int op = pt_slot_op(D, s, j);
+                if (op >= 0 && op < 8) {
+                    if constexpr (has_prev)
+                        if ((op >> 1) < MB) vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
+                } else if (op >= 8) {
+                    if constexpr (has_next)
+                        if (op - 8 < KS) kk[(op - 8) % KS] = kop_at(slot_nx, par_n, op - 8);
+                }
+            }
+        };
+        auto mf_slot = [&](int s) {  // slot s's MFMAs
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int op = pt_slot_op(D, s, j);
+                if (op >= 0 && op < 8) {
+                    if constexpr (has_prev)
+                        if ((op >> 1) < MB) {
+                            const int m = (op >> 1) % MB;
+                            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][op & 1], pp[op & 1], o[m], 0, 0, 0);
+                        }
+                } else if (op >= 8) {
+                    if constexpr (has_next)
+                        if (op - 8 < KS) qk(kk[(op - 8) % KS], op - 8);
+                }
+            }
+        };
+        float x[16], p[16], q[16];
+        auto exps = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) p[r] = __builtin_amdgcn_exp2f(x[r]);
+        };
+        auto quant = [&](int r0, int r1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
+        };
+        auto perms = [&](int j0, int j1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j >= j0 && j < j1) {
+                    const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(q[2 * j + 1]),
+                                                                               __float_as_uint(q[2 * j]), 0x05040100u));
+                    pc[j >> 2][2 * (j & 3)] = h2[0];
+                    pc[j >> 2][2 * (j & 3) + 1] = h2[1];
+                }
+            asm volatile("" : "+v"(pc[0]), "+v"(pc[1]));  // no IR-level sinking past this region
+        };
+        rd_slot(0);
+        rd_slot(1);
+        QMHA_FENCE();
+        // ---- R0: the tile head (quarter-rate / transcendental), then O *= alpha of tile t-1
+        head(s_cur, t);
+        const float c = h_c, kn = h_k;
+        QMHA_FENCE();
+        if constexpr (has_prev) {
+            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        pin_regs(x, 0, 8);
+        QMHA_FENCE();
+        mf_slot(0);
+        QMHA_FENCE();
+        // ---- R1
+        exps(0, 4);
+        QMHA_FENCE();
+        rd_slot(2);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
+        pin_regs(x, 8, 16);
+        quant(0, 4);
+        float rs0 = (p[0] + p[1]) + (p[2] + p[3]);
+        asm volatile("" : "+v"(rs0));
+        QMHA_FENCE();
+        mf_slot(1);
+        QMHA_FENCE();
+        // ---- R2
+        exps(4, 8);
+        perms(0, 2);
+        QMHA_FENCE();
+        rd_slot(3);
+        quant(4, 8);
+        float rs1 = (p[4] + p[5]) + (p[6] + p[7]);
+        asm volatile("" : "+v"(rs1));
+        QMHA_FENCE();
+        mf_slot(2);
+        QMHA_FENCE();
+        // ---- R3
+        exps(8, 12);
+        perms(2, 4);
+        QMHA_FENCE();
+        rd_slot(4);
+        quant(8, 12);
+        float rs2 = (p[8] + p[9]) + (p[10] + p[11]);
+        asm volatile("" : "+v"(rs2));
+        QMHA_FENCE();
+        mf_slot(3);
+        QMHA_FENCE();
+        // ---- R4
+        exps(12, 16);
+        perms(4, 6);
+        QMHA_FENCE();
+        rd_slot(5);
+        quant(12, 16);
+        float rs3 = (p[12] + p[13]) + (p[14] + p[15]);
+        asm volatile("" : "+v"(rs3));
+        QMHA_FENCE();
+        mf_slot(4);
+        QMHA_FENCE();
+        // ---- R5
+        perms(6, 8);
+        QMHA_FENCE();
+        l_run = fmaf(h_alpha, l_run, ((rs0 + rs1) + (rs2 + rs3)) * h_f);  // l = alpha l + sum(p)
+        m_run = h_m;
+        QMHA_FENCE();
+        mf_slot(5);
+        QMHA_FENCE();
+        pp[0] = pc[0];
+        pp[1] = pc[1];
+        alpha_prev = h_alpha;
+        if constexpr (has_next) s_cur = s_nxt;
+    };
+    auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
+        if constexpr (TSHADOW)
+            iter_ts(t, HP, HN, PH);
+        else if constexpr (PT)
+            iter_pt(t, HP, HN, PH);
+        else
+            iter(t, HP, HN, PH);
+    };
+    using T1 = std::integral_constant<bool, true>;
+    using F0 = std::integral_constant<bool, false>;
+    // G >= 2 (the per-block launcher routes N < 64 elsewhere): first, interior, last tile; G == 1
+    // (the per-tensor mode at N = 32): one tile, its P@V in the drain
+    using DYN = std::integral_constant<int, -1>;
+    if (PT && G == 1) {
+        if constexpr (PT) run_iter(0, F0{}, F0{}, DYN{});
+    } else {
+    // FL_FAIR: a workgroup's waves lower their issue priority as their sweep progresses (3 in the
+    // first quarter of the tiles .. 0 in the last), so the co-resident workgroups of a SIMD -- which
+    // the age-ordered arbiter would otherwise finish one after another -- advance together and the
+    // kernel does not end on a few workgroups running alone (tools/timeline.py)
+    auto set_prio = [&](int tt) {
+        if constexpr (FAIR) {
+            const int q = (4 * tt) / G;  // wave-uniform
+            if (q <= 0)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+    };
+    set_prio(0);
+    run_iter(0, F0{}, T1{}, DYN{});
+    int t = 1;
+    constexpr int PER = 2 * RING;  // ring period in tiles
+    for (; t + PER <= G - 1; t += PER) {
+        set_prio(t);
+        run_iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
+        run_iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
+        run_iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
+        run_iter(t + 3, T1{}, T1{}, std::integral_constant<int, 3>{});
+        run_iter(t + 4, T1{}, T1{}, std::integral_constant<int, 4>{});
+        run_iter(t + 5, T1{}, T1{}, std::integral_constant<int, 5>{});
+        if constexpr (RING4) {
+            run_iter(t + 6, T1{}, T1{}, std::integral_constant<int, 6>{});
+            run_iter(t + 7, T1{}, T1{}, std::integral_constant<int, 7>{});
+        }
+    }
+    for (; t < G - 1; ++t) run_iter(t, T1{}, T1{}, DYN{});
+    run_iter(G - 1, T1{}, F0{}, DYN{});
+    }
+#undef QMHA_FENCE
+    // drain: P@V of the last tile (TSHADOW: first the pending d-block-1 fold of tile G-2)
+    {
+        const int t = G - 1;
+        if constexpr (TSHADOW) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[1][r] = fmaf(a[1][r], scale_pp, o[1][r]);
+        }
+        if constexpr (PT) {
+            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {  // O still owes the last tile's alpha
+#pragma unroll
+                for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
+            }
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
+        } else if constexpr (ACC1) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                a[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, 0), pp[0], v16f{}, 0, 0, 0);
+                a[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, 1), pp[1], a[0], 0, 0, 0);
+                o[m] += a[0] * scale_prev;
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] += a[m] * scale_prev;
+        }
+    }
+    // ---- epilogue (fa_tc_int8_b.cu:540-578): out = O / l, 0 if l <= 1e-20
+    // lane (col, half) holds O^T rows d = 32 m + 8 g4 + 4 half + jj of query col
+    if (active) {
+        // PT: O is in units of 2^-24 (the f16-subnormal P entries) times sV / 127: 2^24 * sV / 127
+        // rescales it exactly to the oracle's O * (sV / 127)
+        const float unanchor = PT ? 16777216.0f * (svb[0] / 127.0f) : __builtin_amdgcn_exp2f(anchor - m_run);
+        const float l = PT ? half_swap_add(l_run) : half_swap_add(l_run) * unanchor;
+        const bool ok = l > 1e-20f;
+        float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                v4f w;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) w[jj] = ok ? (o[m][4 * g4 + jj] * unanchor) / l : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 32 * m + 8 * g4) = w;
+            }
+    }
+#ifdef QMHA_TIMELINE
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 17)) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        qmha_tl_buf[0][blockIdx.x] = tl_t0;
+        qmha_tl_buf[1][blockIdx.x] = qmha_tl_now();
+        qmha_tl_buf[2][blockIdx.x] = hw;
+        qmha_tl_buf[3][blockIdx.x] = xcc;
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------------------
+// Debug: the int32 S = Qi Ki^T tiles of one head through the same MFMA operand path
+// (for the bit-exact KAT in tests/).  One wave per 32x32 tile.
+// ---------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void qmha_debug_qk_int32_kernel(const int8_t* __restrict__ Qi, const int8_t* __restrict__ Ki,
+                                                                int N, int bh, int32_t* __restrict__ S) {
+    constexpr int KS = D / 32;
+    const int qg = blockIdx.x, kg = blockIdx.y;
+    const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
+    const int8_t* qp = Qi + ((size_t)bh * N + (size_t)qg * 32 + col) * D + 16 * half;
+    const int8_t* kp = Ki + ((size_t)bh * N + (size_t)kg * 32 + col) * D + 16 * half;
+    v16i s = {};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+        s = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i*>(kp + 32 * ks),
+                                                  *reinterpret_cast<const v4i*>(qp + 32 * ks), s, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S[((size_t)qg * 32 + col) * N + (size_t)kg * 32 + acc_row(r, half)] = s[r];
+}
+
+// ---------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------
+// Production layout: Ki, Vh, sK, sV (the main kernel quantises Q in registers).  with_q adds Qi
+// and sQ at the end for the int32 Q@K^T test hook, whose pre-pass quantises Q too.
+size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    return e + 2 * e + 2 * s + (with_q ? e + s : 0);
+}
+
+Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
+    Int8Workspace w{};
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    char* p = static_cast<char*>(ws);
+    w.Ki = reinterpret_cast<int8_t*>(p);
+    w.Vh = reinterpret_cast<_Float16*>(p + e);
+    w.sK = reinterpret_cast<float*>(p + 3 * e);
+    w.sV = reinterpret_cast<float*>(p + 3 * e + s);
+    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s) : nullptr;
+    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s) : nullptr;
+    return w;
+}
+
+template <int D, int WAVES, int QPW, int SG, int FL, int ABL = 0>
+static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                                 hipStream_t stream) {
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES * QPW - 1) / (WAVES * QPW);
+    const int nwg = B * H * nqb;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;  // inv_sqrt_d: fa_tc_int8_b.cu:587
+    hipLaunchKernelGGL((qmha_fa_int8_kernel<D, WAVES, QPW, SG, FL, ABL>), dim3(nwg), dim3(WAVES * 64), 0, stream, Qf,
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2);
+    return hipGetLastError();
+}
+
+template <int D, int WAVES, int FL, int PAD = 0>
+static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
+                                      int d_model, hipStream_t stream, QkDump dbg = QkDump{}) {
+    const int G = N / QMHA_GROUP;
+    if (G < 2) return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+#ifdef QMHA_ABLATION
+    // occupancy probe: unused dynamic LDS per workgroup caps the workgroups per CU
+    static const int lds_pad = std::getenv("QMHA_INT8_LDS_PAD") ? std::atoi(std::getenv("QMHA_INT8_LDS_PAD")) : 0;
+#else
+    constexpr int lds_pad = 0;
+#endif
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL, PAD>), dim3(B * H * nqb), dim3(WAVES * 64), lds_pad, stream, Qf,
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
+    return hipGetLastError();
+}
+
+// ---- per-tensor mode (fa_tc_int8_pt) -----------------------------------------------------
+size_t int8_pt_workspace_bytes(int B, int N, int H, int D) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t s = align_up((size_t)B * H * sizeof(float), 256);
+    return e + 2 * e + g + 3 * s;
+}
+
+Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D) {
+    const size_t e = align_up((size_t)B * H * N * D, 256);
+    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t s = align_up((size_t)B * H * sizeof(float), 256);
+    char* p = static_cast<char*>(ws);
+    Int8Workspace w{};
+    w.Ki = reinterpret_cast<int8_t*>(p);
+    w.Vh = reinterpret_cast<_Float16*>(p + e);
+    w.gmax = reinterpret_cast<float*>(p + 3 * e);
+    w.sQ = reinterpret_cast<float*>(p + 3 * e + g);
+    w.sK = reinterpret_cast<float*>(p + 3 * e + g + s);
+    w.sV = reinterpret_cast<float*>(p + 3 * e + g + 2 * s);
+    return w;
+}
+
+template <int D, int FL, int WAVES = 4>
+static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                                    hipStream_t stream, QkDump dbg = QkDump{}) {
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ);
+    return hipGetLastError();
+}
+
+// Pipelined-kernel flags at d = 32 and d = 128 (A/B builds may override with -DQMHA_D32_FL=...).
+// d = 128: 4 d-blocks of O and of P@V accumulators -> 2 waves per SIMD, operands read at their MFMA
+#ifndef QMHA_D64_FL
+#define QMHA_D64_FL (FL_MAGIC | FL_KFOLD)
+#endif
+#ifndef QMHA_D32_FL
+#define QMHA_D32_FL (FL_MAGIC | FL_KFOLD)
+#endif
+#ifndef QMHA_D128_FL
+#define QMHA_D128_FL (FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2)
+#endif
+constexpr int kD64Flags = QMHA_D64_FL, kD32Flags = QMHA_D32_FL, kD128Flags = QMHA_D128_FL;
+// per-tensor mode at d = 32: a 4-wave register budget (128 VGPRs; 131 otherwise, i.e. 3 waves/SIMD)
+#ifndef QMHA_PT_D32_EXTRA
+#define QMHA_PT_D32_EXTRA FL_LB4
+#endif
+#ifndef QMHA_PT_D32_WAVES
+#define QMHA_PT_D32_WAVES 4
+#endif
+
+// Default geometry per head size (QMHA_INT8_CFG tuning alternatives: QMHA_ABLATION builds only).
+template <int D>
+static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                            hipStream_t stream) {
+    if constexpr (D == 64) {
+#ifdef QMHA_ABLATION
+        static const int abl = std::getenv("QMHA_INT8_ABL") ? std::atoi(std::getenv("QMHA_INT8_ABL")) : 0;
+        switch (abl) {
+            case 1: return fa_int8_launch<D, 4, 1, 2, 0, 1>(w, Qf, O, B, N, H, d_model, stream);
+            case 2: return fa_int8_launch<D, 4, 1, 2, 0, 2>(w, Qf, O, B, N, H, d_model, stream);
+            case 4: return fa_int8_launch<D, 4, 1, 2, 0, 4>(w, Qf, O, B, N, H, d_model, stream);
+            case 16: return fa_int8_launch<D, 4, 1, 2, 0, 16>(w, Qf, O, B, N, H, d_model, stream);
+            case 64: return fa_int8_launch<D, 4, 1, 2, 0, 64>(w, Qf, O, B, N, H, d_model, stream);
+            case 6: return fa_int8_launch<D, 4, 1, 2, 0, 6>(w, Qf, O, B, N, H, d_model, stream);
+            case 7: return fa_int8_launch<D, 4, 1, 2, 0, 7>(w, Qf, O, B, N, H, d_model, stream);
+            case 70: return fa_int8_launch<D, 4, 1, 2, 0, 70>(w, Qf, O, B, N, H, d_model, stream);
+            case 11000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 10000>(w, Qf, O, B, N, H, d_model, stream);
+            case 14000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ABL_NOMFMA2>(w, Qf, O, B, N, H, d_model, stream);
+            case 15000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ABL_NOEXP>(w, Qf, O, B, N, H, d_model, stream);
+            case 12000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 20000>(w, Qf, O, B, N, H, d_model, stream);
+            case 13000: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD, 30000>(w, Qf, O, B, N, H, d_model, stream);
+            default: break;
+        }
+        // tuning alternatives (profiling builds only: the production library has one kernel per d)
+        switch (tune_config("QMHA_INT8_CFG")) {
+            case 4120: return fa_int8_launch<D, 4, 1, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 4122: return fa_int8_launch<D, 4, 1, 2, FL_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
+            case 4125: return fa_int8_launch<D, 4, 1, 2, FL_MAGIC | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 4220: return fa_int8_launch<D, 4, 2, 2, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 9040: return fa_int8_pipe_launch<D, 4, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 9080: return fa_int8_pipe_launch<D, 8, 0>(w, Qf, O, B, N, H, d_model, stream);
+            case 9048: return fa_int8_pipe_launch<D, 4, FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
+            case 9064: return fa_int8_pipe_launch<D, 4, FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9044: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
+            case 9049: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_EARLY | FL_JIT>(w, Qf, O, B, N, H, d_model, stream);
+            case 9041: return fa_int8_pipe_launch<D, 4, FL_MAGIC>(w, Qf, O, B, N, H, d_model, stream);
+            case 9043: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_EARLY>(w, Qf, O, B, N, H, d_model, stream);
+            // workgroup size: each LDS-DMA stage shared by more waves (fewer pieces per wave)
+            case 9061: return fa_int8_pipe_launch<D, 6, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9081: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9121: return fa_int8_pipe_launch<D, 12, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            case 9021: return fa_int8_pipe_launch<D, 2, FL_MAGIC | FL_KFOLD>(w, Qf, O, B, N, H, d_model, stream);
+            // 4 waves/SIMD budget (operands read at their MFMA): 4- and 8-wave workgroups, the latter
+            // sharing each LDS-DMA stage between 8 waves at the same occupancy
+            case 9141: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9181: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            // one P@V accumulator block (FL_ACC1): at the default budget, and at 4 waves/SIMD with 4- / 8-wave workgroups
+            case 9200: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ACC1>(w, Qf, O, B, N, H, d_model, stream);
+            case 9241: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_ACC1 | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            case 9281: return fa_int8_pipe_launch<D, 8, FL_MAGIC | FL_KFOLD | FL_ACC1 | FL_JIT | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            // MFMA shadows filled with transcendental / quarter-rate work (FL_TSHADOW)
+            case 9300: return fa_int8_pipe_launch<D, 4, FL_MAGIC | FL_KFOLD | FL_TSHADOW>(w, Qf, O, B, N, H, d_model, stream);
+            default: break;
+        }
+#endif
+        // default at d = 64: the software-pipelined kernel with the folded score bias
+        // (KFOLD: -2 % against plain MAGIC on one box, profiles/r01/overlap_sweep.txt)
+        return fa_int8_pipe_launch<D, 4, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
+    }
+    if constexpr (D == 32) {
+#ifdef QMHA_ABLATION
+        // workgroup size at d = 32 (122 VGPRs: 4 waves/SIMD, so an 8-wave workgroup keeps full
+        // occupancy, unlike d = 64): each LDS-DMA stage shared by more waves
+        static const int abl32 = std::getenv("QMHA_INT8_ABL") ? std::atoi(std::getenv("QMHA_INT8_ABL")) : 0;
+        switch (abl32) {
+            case 32081: return fa_int8_pipe_launch<D, 8, kD32Flags | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 32061: return fa_int8_pipe_launch<D, 6, kD32Flags | FL_LB2>(w, Qf, O, B, N, H, d_model, stream);
+            case 32041: return fa_int8_pipe_launch<D, 4, kD32Flags | FL_LB4>(w, Qf, O, B, N, H, d_model, stream);
+            default: break;
+        }
+#endif
+        return fa_int8_pipe_launch<D, 4, kD32Flags>(w, Qf, O, B, N, H, d_model, stream);
+    }
+    return fa_int8_pipe_launch<D, 4, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
+}
+
+hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return fa_int8_pt_launch<32, kD32Flags | QMHA_PT_D32_EXTRA, QMHA_PT_D32_WAVES>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, hipStream_t stream) {
+    switch (D) {
+        case 32: return fa_int8_d<32>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_d<64>(w, Qf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_d<128>(w, Qf, O, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The production int8 schedule with FL_DUMP: same kernel template, same flags plus the stores
+// of what it computed (S^T per tile, Q operand, sQ), at every head size.
+hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                               int d_model, QkDump dbg, hipStream_t stream) {
+    if (N / QMHA_GROUP < 2) return hipErrorInvalidValue;
+    switch (D) {  // the production flags of fa_int8_d, plus FL_DUMP
+        case 32: return fa_int8_pipe_launch<32, 4, kD32Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 64: return fa_int8_pipe_launch<64, 4, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 128:
+            return fa_int8_pipe_launch<128, 4, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The per-tensor mode's production schedule with FL_DUMP (same flags and workgroup size as
+// launch_fa_int8_pt_main, plus the stores)
+hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
+                                  int d_model, QkDump dbg, hipStream_t stream) {
+    switch (D) {
+        case 32:
+            return fa_int8_pt_launch<32, kD32Flags | QMHA_PT_D32_EXTRA | FL_DUMP, QMHA_PT_D32_WAVES>(w, Qf, O, B, N, H,
+                                                                                                 d_model, stream, dbg);
+        case 64: return fa_int8_pt_launch<64, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 128: return fa_int8_pt_launch<128, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream) {
+    const int G = N / QMHA_GROUP;
+    switch (D) {
+        case 32: hipLaunchKernelGGL((qmha_debug_qk_int32_kernel<32>), dim3(G, G), dim3(64), 0, stream, w.Qi, w.Ki, N, bh, S); break;
+        case 64: hipLaunchKernelGGL((qmha_debug_qk_int32_kernel<64>), dim3(G, G), dim3(64), 0, stream, w.Qi, w.Ki, N, bh, S); break;
+        case 128: hipLaunchKernelGGL((qmha_debug_qk_int32_kernel<128>), dim3(G, G), dim3(64), 0, stream, w.Qi, w.Ki, N, bh, S); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace qmha
