@@ -60,11 +60,23 @@ __device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void*
 
 // Per-tensor mode (fa_tc_int8_pt): the scale of a head's whole [N, d] slice from the absmax of
 // its G 32-row groups (qmha_group_absmax_kernel): max is exact in any order, so this equals the
-// fp32_to_int8sram arithmetic over the whole slice (fa_tc_int8_b.cu:56-106)
-__device__ __forceinline__ float slice_scale(const float* __restrict__ gmax, int G, int lane) {
+// fp32_to_int8sram arithmetic over the whole slice (fa_tc_int8_b.cu:56-106).  One wave per
+// (tensor, bh) slice reads its G group maxima once and writes the slice scale to s{Q,K,V}[bh]
+// (round-3 ADVICE: every quantising wave used to re-reduce all G maxima of its slice, G^2 reads
+// per slice -- 16 MB per slice and tensor at N = 65536).
+__global__ __launch_bounds__(256) void qmha_slice_scale_kernel(const float* __restrict__ gmax, float* __restrict__ sQ,
+                                                               float* __restrict__ sK, float* __restrict__ sV, int BH,
+                                                               int G, int first_tensor) {
+    const int tensor = blockIdx.y + first_tensor;
+    const int lane = threadIdx.x & 63;
+    const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (bh >= BH) return;  // wave-uniform
+    const float* gm = gmax + ((size_t)tensor * BH + bh) * G;
     float m = 0.0f;
-    for (int i = lane; i < G; i += 64) m = fmaxf(m, gmax[i]);
-    return qmha_scale_from_absmax(wave_max64(m));
+    for (int i = lane; i < G; i += 64) m = fmaxf(m, gm[i]);
+    const float sc = qmha_scale_from_absmax(wave_max64(m));
+    float* s_out = tensor == 0 ? sQ : (tensor == 1 ? sK : sV);
+    if (lane == 0 && s_out) s_out[bh] = sc;
 }
 
 // One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
@@ -100,15 +112,14 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
 // Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
 // One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
 // ---------------------------------------------------------------------------------------
-// PT (per-tensor mode): gmax = [3][B*H][G] group absmax of Q, K, V (qmha_group_absmax_kernel);
-// every group of a head slice is quantised with the slice's scale; the group-0 wave of each
-// slice writes that scale to s{Q,K,V}[bh]
+// PT (per-tensor mode): every group of a head slice is quantised with the slice's scale, read from
+// s{K,V}[bh] (qmha_slice_scale_kernel)
 template <int D, int VMODE, bool PT = false>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
     float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
-    int N, int H, int d_model, int total_groups, int first_tensor, const float* __restrict__ gmax = nullptr) {
+    int N, int H, int d_model, int total_groups, int first_tensor) {
     __shared__ __attribute__((aligned(16))) char vtr[4][D * QMHA_VT_PITCH];
     const int tensor = blockIdx.y + first_tensor;
     const int lane = threadIdx.x & 63;
@@ -119,15 +130,7 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const int bh = item / G, g = item % G;
     const int b = bh / H, k = bh % H;
     float slice_sc = 0.0f;
-    if constexpr (PT) {
-        slice_sc = slice_scale(gmax + ((size_t)tensor * total_groups + (size_t)bh * G), G, lane);
-        float* s_out = tensor == 0 ? sQ : (tensor == 1 ? sK : sV);
-        if (g == 0 && lane == 0 && s_out) s_out[bh] = slice_sc;
-        if (tensor == 1 && g == 0 && sQ) {  // Q is quantised by the main kernel: its slice scale from here
-            const float sq = slice_scale(gmax + (size_t)bh * G, G, lane);
-            if (lane == 0) sQ[bh] = sq;
-        }
-    }
+    if constexpr (PT) slice_sc = (tensor == 0 ? sQ : (tensor == 1 ? sK : sV))[bh];
     if (tensor == 2)
         quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model, slice_sc);
     else
@@ -334,27 +337,40 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
 // slice scales.  (r03: batch chunks of ~96 MiB of K + V, each absmax pass followed at once by its
 // quantisation so the re-read of K / V could come from the Infinity Cache, measured 0.260 against
 // 0.230 ms at C4, profiles/r03/pt/ab_chunk/)
+// Three launches over the whole batch: the group absmax of Q, K, V (reads the fp32 tensors once),
+// the slice scales, then K / V quantised with them (reads K / V again: 1.54 GB per call at C4, at
+// the HBM roofline).  r03: batch chunks of ~96 MiB of K + V, each absmax pass followed at once by
+// its quantisation so the re-read could come from the Infinity Cache, measured 0.260 against 0.230
+// ms (profiles/r03/pt/ab_chunk/); r04: one workgroup per head slice doing both passes back to back
+// (re-read from the cache) measured 0.270 ms: one workgroup per 1 MiB slice is latency-bound
+// (3.7 TB/s on its 1.0 GB of HBM traffic; profiles/r04/ab_pt_prepass/)
 template <int D>
 static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                   int H, int d_model, hipStream_t stream) {
-    const int total = B * H * (N / QMHA_GROUP);
+    const int G = N / QMHA_GROUP, BH = B * H;
+    const int total = BH * G;
     hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.gmax, N,
                        H, d_model, total);
+    hipLaunchKernelGGL(qmha_slice_scale_kernel, dim3((BH + 3) / 4, 3), dim3(256), 0, stream, (const float*)w.gmax, w.sQ,
+                       w.sK, w.sV, BH, G, 0);
     // K and V quantised with their slice scales (blockIdx.y = tensor - 1); Q by the main kernel
     hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V,
-                       nullptr, w.Ki, (void*)w.Vh, w.sQ, w.sK, w.sV, N, H, d_model, total, 1, (const float*)w.gmax);
+                       nullptr, w.Ki, (void*)w.Vh, w.sQ, w.sK, w.sV, N, H, d_model, total, 1);
     return hipGetLastError();
 }
 
 template <int D>
 static hipError_t quant_int8_pt_rows_d(const float* X, const Int8Workspace& w, int B, int N, int H, int d_model,
                                        hipStream_t stream) {
-    const int total = B * H * (N / QMHA_GROUP);
-    // X in the K role (tensor 1) of a [3][B*H][G] gmax table: absmax, then int8 rows + slice scales
+    const int G = N / QMHA_GROUP, BH = B * H;
+    const int total = BH * G;
+    // X in the K role (tensor 1) of a [3][B*H][G] gmax table: absmax, slice scales, then int8 rows
     hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X, w.gmax, N,
                        H, d_model, total, 1);
+    hipLaunchKernelGGL(qmha_slice_scale_kernel, dim3((BH + 3) / 4, 1), dim3(256), 0, stream, (const float*)w.gmax, nullptr,
+                       w.sK, nullptr, BH, G, 1);
     hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X,
-                       nullptr, w.Ki, nullptr, nullptr, w.sK, nullptr, N, H, d_model, total, 1, (const float*)w.gmax);
+                       nullptr, w.Ki, nullptr, nullptr, w.sK, nullptr, N, H, d_model, total, 1);
     return hipGetLastError();
 }
 

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--H", type=int, default=16)
     ap.add_argument("--N", type=int, default=4096)
     ap.add_argument("--d", type=int, default=64)
+    ap.add_argument("--bursts", default="batched,async1,solve,batched_again,ref",
+                    help="comma-separated subset of batched, async1, solve, batched_again, ref")
     a = ap.parse_args()
     lib = _lib.load()
     vid = _lib.variant_id(a.variant)
@@ -71,12 +73,15 @@ def main():
             _lib.check(lib.qmha_solve_variant(Q.data_ptr() + b * sz, K.data_ptr() + b * sz, V.data_ptr() + b * sz,
                                               O.data_ptr() + b * sz, N, H * d, H, vid))
 
+    sel = set(a.bursts.split(","))
     for _ in range(20):  # clock ramp
         batched()
-    burst("batched", batched, a.reps)
-    burst("async1", async1, a.reps)
-    burst("solve", solve_calls, a.reps)
-    burst("batched_again", batched, a.reps)
+    for name, fn in (("batched", batched), ("async1", async1), ("solve", solve_calls), ("batched_again", batched)):
+        if name in sel:
+            burst(name, fn, a.reps)
+    if "ref" not in sel:
+        print(json.dumps(res))
+        return
     # the reference's own shape at B = 1, 2, 4 (per-sequence throughput vs grid fill)
     del Q, K, V, O
     for Bn in (1, 2, 4):
