@@ -34,10 +34,7 @@ static constexpr float kLog2eH = 1.4426950408889634f;
 enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16, F16_LB1 = 32 };
 
 template <int D, int WAVES, int SG, int FL>
-#ifndef QMHA_F16_LBN
-#define QMHA_F16_LBN 4  // waves per SIMD of the F16_LB4 budget (A/B builds: 5, 6)
-#endif
-__global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? QMHA_F16_LBN : ((FL & F16_LB1) ? 1 : 2)) void qmha_fa_f16_v2_kernel(
+__global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 1 : 2)) void qmha_fa_f16_v2_kernel(
     const float* __restrict__ Qf, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     QMHA_ENABLE_AGPR_MFMA();
