@@ -44,6 +44,12 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 #define I_CMPS(i) "v_cmp_lt_f32 vcc, %18, %" #i "\n\t"
 #define I_CMPV(i) "v_cmp_lt_f32 vcc, %16, %" #i "\n\t"
 #define I_FMA_MIX(i) "v_fma_mix_f32 %" #i ", %" #i ", %16, %17\n\t"
+// r04: ways to pack the low 16 bits of two registers (the int8 kernel's f16-subnormal P operand pairs)
+#define I_SDWA(i) "v_mov_b32_sdwa %" #i ", %16 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0\n\t"
+#define I_PACKF16(i) "v_pack_b32_f16 %" #i ", %" #i ", %16\n\t"
+#define I_LSHLOR(i) "v_lshl_or_b32 %" #i ", %16, 16, %" #i "\n\t"
+#define I_BFI(i) "v_bfi_b32 %" #i ", %17, %" #i ", %16\n\t"
+#define I_ADDSDWA(i) "v_add_f32_sdwa %" #i ", %" #i ", %16 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t"
 
 #define P8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define I_PKFMA(i) "v_pk_fma_f32 %" #i ", %" #i ", %8, %9\n\t"
@@ -55,7 +61,8 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 enum {
     OP_FMA, OP_FMAC, OP_ADD, OP_MUL, OP_EXP, OP_MAX, OP_MAX3, OP_MAXI, OP_PERM, OP_CVT, OP_MOV, OP_FMAAK, OP_DPP, OP_PL,
     OP_SUB, OP_ADDU, OP_FMAS, OP_CVTPK, OP_RCP, OP_MAX3I, OP_FMAMIX, OP_PKFMA, OP_PKFMAB, OP_PKADD, OP_PKMUL, OP_PKMOV,
-    OP_MULS, OP_FMACS, OP_ADDS, OP_CMPS, OP_CMPV, OP_MFMA16, OP_MFMA8, OP_N
+    OP_MULS, OP_FMACS, OP_ADDS, OP_CMPS, OP_CMPV, OP_SDWA, OP_PACKF16, OP_LSHLOR, OP_BFI, OP_ADDSDWA, OP_MFMA16, OP_MFMA8,
+    OP_N
 };
 static const char* kNames[OP_N] = {
     "v_fma_f32", "v_fmac_f32", "v_add_f32", "v_mul_f32", "v_exp_f32", "v_max_f32", "v_max3_f32", "v_max_i32",
@@ -63,6 +70,7 @@ static const char* kNames[OP_N] = {
     "v_add_u32", "v_fma_f32 (sgpr)", "v_cvt_pk_f16_f32", "v_rcp_f32", "v_max3_i32", "v_fma_mix_f32", "v_pk_fma_f32",
     "v_pk_fma_f32 bcast", "v_pk_add_f32", "v_pk_mul_f32", "v_pk_mov_b32", "v_mul_f32 (sgpr, vop2)",
     "v_fmac_f32 (sgpr, vop2)", "v_add_f32 (sgpr, vop2)", "v_cmp_lt_f32 (sgpr)", "v_cmp_lt_f32 (vgpr)",
+    "v_mov_b32_sdwa WORD_1", "v_pack_b32_f16", "v_lshl_or_b32", "v_bfi_b32", "v_add_f32_sdwa",
     "mfma_f32_32x32x16_f16", "mfma_i32_32x32x32_i8"};
 
 template <int OP>
@@ -108,6 +116,11 @@ __device__ float body(float seed, float sx) {
         if constexpr (OP == OP_ADDS) ASM16(I_ADDS);
         if constexpr (OP == OP_CMPS) asm volatile(R16(I_CMPS) : OUTS16 : "v"(x), "v"(y), "s"(sx) : "vcc");
         if constexpr (OP == OP_CMPV) asm volatile(R16(I_CMPV) : OUTS16 : "v"(x), "v"(y), "s"(sx) : "vcc");
+        if constexpr (OP == OP_SDWA) ASM16(I_SDWA);
+        if constexpr (OP == OP_PACKF16) ASM16(I_PACKF16);
+        if constexpr (OP == OP_LSHLOR) ASM16(I_LSHLOR);
+        if constexpr (OP == OP_BFI) ASM16(I_BFI);
+        if constexpr (OP == OP_ADDSDWA) ASM16(I_ADDSDWA);
         if constexpr (OP == OP_PKFMA) { ASM8P(I_PKFMA); ASM8P(I_PKFMA); }
         if constexpr (OP == OP_PKFMAB) { ASM8P(I_PKFMAB); ASM8P(I_PKFMAB); }
         if constexpr (OP == OP_PKADD) { ASM8P(I_PKADD); ASM8P(I_PKADD); }
