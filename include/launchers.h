@@ -144,11 +144,6 @@ void qmha_profile_enable(int on);
 /* Number of batch chunks for the pre-pass / main-kernel overlap (1..16, 1 = off); returns the
  * previous value.  Results are bit-identical for every setting. */
 int qmha_set_overlap_chunks(int n);
-/* Schedule of the fa_tc_int8_b main kernel at d = 32 / 64 (a test / A/B hook; results are
- * bit-identical for every setting): 0 = automatic (the head-ahead schedule for grids of at most two
- * waves per SIMD, e.g. one C4 sequence per call; the three-wave schedule otherwise), 1 = always the
- * three-wave schedule, 2 = always head-ahead.  Returns the previous value, -1 for an unknown mode. */
-int qmha_set_int8_schedule(int mode);
 int qmha_profile_collect(double *main_ms, long long *launches, double *prepass_ms);
 
 /* Release all library-owned workspaces (optional; also released at process exit). */

@@ -35,7 +35,6 @@ SIGNATURES = {
     "qmha_last_error": (_cp, []),
     "qmha_profile_enable": (None, [_i]),
     "qmha_set_overlap_chunks": (_i, [_i]),
-    "qmha_set_int8_schedule": (_i, [_i]),
     "qmha_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                   ctypes.POINTER(ctypes.c_double)]),
     "qmha_release_workspaces": (None, []),

@@ -526,13 +526,6 @@ int qmha_set_overlap_chunks(int n) {
     return prev;
 }
 
-int qmha_set_int8_schedule(int mode) {
-    static std::atomic<int> cur{0};
-    if (mode < 0 || mode > 2) return -1;
-    qmha::set_int8_schedule(mode);
-    return cur.exchange(mode);
-}
-
 void qmha_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;

@@ -36,7 +36,6 @@
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
-#include <atomic>
 #include <type_traits>
 
 namespace qmha {
@@ -101,10 +100,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //             removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump: the bit-exact
 //             check of the production Q@K^T path; never the production launch)
 //   FL_PT     (pipe kernel) the per-tensor mode fa_tc_int8_pt
-//   FL_HA     (pipe kernel, per-block, d = 32 / 64, with FL_LB2) the under-filled-grid schedule: the tile
-//             head computed one tile ahead, beside the previous tile's softmax
-enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576,
-       FL_HA = 2097152 };
+enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576 };
 
 // ---------------------------------------------------------------------------------------
 // One-tile-at-a-time main kernel (every head size; N = 32).
@@ -350,15 +346,6 @@ __host__ __device__ constexpr int pt_slot_op(int D, int s, int j) {
     return D == 32 ? d32[s][j] : D == 64 ? d64[s][j] : d128[s][j];
 }
 
-// FL_HA's MFMA placement, same op codes as pt_slot_op: Q@K^T of tile t+1 right after the first two
-// VALU regions (its scores feed the head of t+1 in region 4), P@V of tile t-1 in regions 2..5
-// (every chained pair two regions apart)
-__host__ __device__ constexpr int ha_slot_op(int D, int s, int j) {
-    constexpr int d32[6][2] = {{8, -1}, {-1, -1}, {0, -1}, {-1, -1}, {1, -1}, {-1, -1}};
-    constexpr int d64[6][2] = {{8, -1}, {9, -1}, {0, -1}, {2, -1}, {1, -1}, {3, -1}};
-    return D == 32 ? d32[s][j] : d64[s][j];
-}
-
 template <int N>
 __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
 #pragma unroll
@@ -371,7 +358,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
-    const float* __restrict__ sQt = nullptr) {
+    const float* __restrict__ sQt = nullptr, int fair = 0) {
     constexpr int SG = 2, RING = 3, PF = RING - 1;  // PF: stages in flight ahead
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
@@ -872,180 +859,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         alpha_prev = h_alpha;
         if constexpr (has_next) s_cur = s_nxt;
     };
-    // ---- FL_HA: the per-block iteration for grids of at most two waves per SIMD (one C4 sequence per
-    // call: 2048 waves on 1024 SIMDs).  There the shipped order -- the tile head (row max, running max,
-    // P-tile max, sP, 1/sP: a serial chain of ~40 dependent VALU / DPP / permlane / transcendental
-    // steps) first, then the tile's softmax that depends on it -- leaves each wave stalled on that
-    // chain with no third wave to cover it.  FL_HA computes the head of tile t+1 in iteration t,
-    // interleaved with tile t's P quantisation: Q@K^T of t+1 issues first in the iteration, so its
-    // scores have landed by region 4, and the head needs only them and tile t's running max.  Every
-    // tile's arithmetic, and the order in which the tiles fold into O and l, are the shipped
-    // kernel's, so the output is bit-identical to it (tests: test_int8_head_ahead_bit_identical).
-    // Register budget: two waves per SIMD (FL_LB2); the launcher picks it only for such grids.
-    struct TileHead {
-        float c, m, k, f, sp, invp;
-    };
-    auto head_of = [&](const v16i& s, int t, float m_prev) {  // = head() above, per-block, into a struct
-        TileHead h;
-        float c = cq * skb[t];
-        const int mxi = half_swap_max_i(tree_max16_i(s));
-        c = __int_as_float((__float_as_int(c) + 2) & ~3);
-        const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;
-        h.m = fmaxf(m_prev, sfmax * c);
-        h.k = fmaf(c, QMHA_MAGIC_RNE, h.m);
-        const float delta = fmaf(c, -QMHA_MAGIC_RNE, h.k) - h.m;
-        h.f = fmaf(delta, 0.69314718055994531f, 1.0f);
-        const float xmax = fmaf(sfmax, c, -h.m);
-        h.c = c;
-        const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
-        const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
-        h.invp = __builtin_amdgcn_rcpf(sp);
-        h.invp *= h.f;
-        h.sp = sp * 16777216.0f;
-        return h;
-    };
-    TileHead hc{}, hn{};  // heads of tiles t (current) and t+1 (next)
-    auto iter_ha = [&](int t, auto HP, auto HN, auto PH) {
-        constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
-        constexpr int ph = decltype(PH)::value;
-        const int odd = ph >= 0 ? ((1 + ph) & 1) : (t & 1);
-        const int slot_p = ph >= 0 ? ((ph >> 1) % RING) : (((t - 1) >> 1) % RING);
-        const int par_p = ph >= 0 ? (ph & 1) : ((t - 1) & 1);
-        const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
-        const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
-        const int dma_st = (t >> 1) + PF;
-        const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
-        if (odd) {  // uniform
-            qmha_dma_barrier();  // stage (t+1)/2 landed; the stage (t-3)/2 slot is free
-            if (dma_st < nst) issue_at(dma_st, dma_slot);
-        }
-        if constexpr (DUMP) {
-            if (active) {
-                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + col) * N + (size_t)t * QMHA_GROUP;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sd[acc_row(r, half)] = s_cur[r] - 0x4B400000;
-            }
-        }
-        v8h vv[MB][2];
-        v4i kk[KS];
-        auto rd_slot = [&](int s) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int op = ha_slot_op(D, s, j);
-                if (op >= 0 && op < 8) {
-                    if constexpr (has_prev)
-                        if ((op >> 1) < MB) vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
-                } else if (op >= 8) {
-                    if constexpr (has_next)
-                        if (op - 8 < KS) kk[(op - 8) % KS] = kop_at(slot_nx, par_n, op - 8);
-                }
-            }
-        };
-        auto mf_slot = [&](int s) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int op = ha_slot_op(D, s, j);
-                if (op >= 0 && op < 8) {
-                    if constexpr (has_prev)
-                        if ((op >> 1) < MB) {
-                            const int m = (op >> 1) % MB, ks = op & 1;
-                            a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][ks], pp[ks], ks == 0 ? v16f{} : a[m], 0, 0, 0);
-                        }
-                } else if (op >= 8) {
-                    if constexpr (has_next)
-                        if (op - 8 < KS) qk(kk[(op - 8) % KS], op - 8);
-                }
-            }
-        };
-        float x[16], p[16];
-        auto quant_pack = [&](int j0, int j1) {  // Pi = rint(p/sP) as f16 subnormals, pairs j0..j1-1 (F above)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j >= j0 && j < j1) {
-                    const float t0 = fmaf(p[2 * j], hc.invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * j + 1], hc.invp, QMHA_MAGIC_RNE);
-                    const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
-                    pc[j >> 2][2 * (j & 3)] = h2[0];
-                    pc[j >> 2][2 * (j & 3) + 1] = h2[1];
-                }
-        };
-        rd_slot(0);
-        rd_slot(1);
-        QMHA_FENCE();
-        // ---- R0: re-anchor (rare) before this tile's shift is formed; scores of rows 0..7
-        if (__builtin_amdgcn_ballot_w64(hc.m - anchor > 48.0f)) {
-            const float f = __builtin_amdgcn_exp2f(anchor - hc.m);
-#pragma unroll
-            for (int m = 0; m < MB; ++m) o[m] *= f;
-            l_run *= f;
-            scale_prev *= f;
-            anchor = hc.m;
-        }
-        const float e = __builtin_amdgcn_exp2f(hc.m - anchor);
-        m_run = hc.m;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), hc.c, -hc.k);
-        QMHA_FENCE();
-        mf_slot(0);
-        QMHA_FENCE();
-        // ---- R1: scores of rows 8..15
-        rd_slot(2);
-#pragma unroll
-        for (int r = 8; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), hc.c, -hc.k);
-        QMHA_FENCE();
-        mf_slot(1);
-        QMHA_FENCE();
-        // ---- R2, R3: p = exp2
-        rd_slot(3);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
-        QMHA_FENCE();
-        mf_slot(2);
-        QMHA_FENCE();
-        rd_slot(4);
-#pragma unroll
-        for (int r = 8; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(x[r]);
-        QMHA_FENCE();
-        mf_slot(3);
-        QMHA_FENCE();
-        // ---- R4: the head of tile t+1 beside the quantisation of rows 0..7
-        rd_slot(5);
-        if constexpr (has_next) hn = head_of(s_nxt, t + 1, hc.m);
-        quant_pack(0, 4);
-        QMHA_FENCE();
-        mf_slot(4);
-        QMHA_FENCE();
-        // ---- R5: rows 8..15, row sum (unquantised p, :336)
-        quant_pack(4, 8);
-        const float rs = tree_sum16(p);
-        QMHA_FENCE();
-        mf_slot(5);
-        QMHA_FENCE();
-        // ---- R6: anchored l, this tile's O scale, fold of tile t-1's P@V into O
-        l_run = fmaf(rs, e * hc.f, l_run);
-        const float scale_t = hc.sp * svb[t] * e;
-        if constexpr (has_prev) {
-#pragma unroll
-            for (int m = 0; m < MB; ++m)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
-        }
-        QMHA_FENCE();
-        pp[0] = pc[0];
-        pp[1] = pc[1];
-        scale_prev = scale_t;
-        if constexpr (has_next) {
-            s_cur = s_nxt;
-            hc = hn;
-        }
-    };
-    constexpr bool HA = FL & FL_HA;
-    static_assert(!HA || (!PT && D <= 64), "FL_HA: per-block mode, d = 32 / 64");
-    if constexpr (HA) hc = head_of(s_cur, 0, 0.0f);
     auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
         if constexpr (PT)
             iter_pt(t, HP, HN, PH);
-        else if constexpr (HA)
-            iter_ha(t, HP, HN, PH);
         else
             iter(t, HP, HN, PH);
     };
@@ -1057,10 +873,28 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     if (PT && G == 1) {
         if constexpr (PT) run_iter(0, F0{}, F0{}, DYN{});
     } else {
+        // fair != 0 (grids of at most 8 rounds of workgroups, the launcher's choice): a workgroup's
+        // waves lower their issue priority quarter by quarter of their sweep (3 .. 0), so the
+        // workgroups sharing a SIMD -- which the age-ordered arbiter otherwise finishes one after the
+        // other, the last ones running alone at a fraction of the SIMD's throughput -- advance together
+        // (one C4 sequence per call -3.3 %, the reference's shape -3.7 %)
+        auto set_prio = [&](int tt) {
+            const int q = (4 * tt) / G;  // wave-uniform
+            if (q <= 0)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        };
+        if (fair) set_prio(0);
         run_iter(0, F0{}, T1{}, DYN{});
         int t = 1;
         constexpr int PER = 2 * RING;  // ring period in tiles
         for (; t + PER <= G - 1; t += PER) {
+            if (fair) set_prio(t);
             run_iter(t, T1{}, T1{}, std::integral_constant<int, 0>{});
             run_iter(t + 1, T1{}, T1{}, std::integral_constant<int, 1>{});
             run_iter(t + 2, T1{}, T1{}, std::integral_constant<int, 2>{});
@@ -1173,6 +1007,29 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
     return hipGetLastError();
 }
 
+// Rounds of workgroups a grid of `nwg` takes on this device at the kernel's occupancy (HIP's own
+// occupancy answer, cached per kernel instance and device); 0 if unknown.
+template <int D, int WAVES, int FL>
+static int pipe_rounds(long long nwg) {
+    static int occ[64] = {}, cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (occ[dev] == 0) {
+        int n = 0, c = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, qmha_fa_int8_pipe_kernel<D, WAVES, FL>, WAVES * 64, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0 || c <= 0)
+            return 0;
+        cus[dev] = c;
+        occ[dev] = n;
+    }
+    const long long slots = (long long)occ[dev] * cus[dev];
+    return (int)((nwg + slots - 1) / slots);
+}
+// issue-priority fairness (the kernel's `fair`) for grids of at most this many rounds: measured
+// -3.3 % (one round), -3.7 % (two), -2.4 % (eight, d = 32), and not adopted at C4's 10.7 rounds
+// (profiles/r04/ab_fair/)
+constexpr int kFairMaxRounds = 8;
+
 template <int D, int WAVES, int FL>
 static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H,
                                       int d_model, hipStream_t stream, QkDump dbg = QkDump{}) {
@@ -1180,8 +1037,10 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     if (G < 2) return fa_int8_launch<D, 0>(w, Qf, O, B, N, H, d_model, stream);  // no pipeline to fill
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    const int rounds = pipe_rounds<D, WAVES, FL>((long long)B * H * nqb);
+    const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)nullptr, fair);
     return hipGetLastError();
 }
 
@@ -1214,8 +1073,10 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    const int rounds = pipe_rounds<D, WAVES, FL | FL_PT>((long long)B * H * nqb);
+    const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
-                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ);
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ, fair);
     return hipGetLastError();
 }
 
@@ -1229,44 +1090,11 @@ constexpr int kD128Flags = FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2, kPtD32Extra = 
 template <int D>
 constexpr int kAnyFlags = FL_MAGIC | (D > 128 ? FL_LB1 : FL_LB2);
 
-// Under-filled grids: at most two waves per SIMD, i.e. B*H*N/32 query groups (one wave each)
-// below three per SIMD, run the head-ahead schedule FL_HA at a two-wave register budget (d = 32 / 64).
-// qmha_set_int8_schedule (a test / A/B hook) forces either schedule.
-static std::atomic<int> g_int8_schedule{0};  // 0 auto, 1 the shipped 3-wave schedule, 2 head-ahead
-void set_int8_schedule(int mode) { g_int8_schedule = mode; }
-
-static bool int8_underfilled(int B, int N, int H) {
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    if (cus[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return false;
-        cus[dev] = n;
-    }
-    const long long waves = (long long)B * H * ((N / QMHA_GROUP + 3) / 4) * 4;
-    return waves < 3LL * 4 * cus[dev];  // 4 SIMDs per CU
-}
-
-static bool int8_use_head_ahead(int B, int N, int H, int D) {
-    if (D != 32 && D != 64) return false;
-    if (const int m = g_int8_schedule.load()) return m == 2;
-    return int8_underfilled(B, N, H);
-}
-
 template <int D, int XFL = 0>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream, QkDump dbg = QkDump{}) {
-    constexpr int kHaFlags = FL_HA | FL_LB2;
-    if constexpr (D == 32) {
-        if (int8_use_head_ahead(B, N, H, D))
-            return fa_int8_pipe_launch<D, 4, kD32Flags | kHaFlags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-        return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    } else if constexpr (D == 64) {
-        if (int8_use_head_ahead(B, N, H, D))
-            return fa_int8_pipe_launch<D, 4, kD64Flags | kHaFlags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-        return fa_int8_pipe_launch<D, 4, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    }
+    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 64) return fa_int8_pipe_launch<D, 4, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }

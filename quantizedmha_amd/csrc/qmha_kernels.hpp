@@ -47,8 +47,6 @@ hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float
 // Qf: the caller's fp32 Q (the main kernel quantises each Q group into its MFMA operand)
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream);
-// 0 automatic, 1 the three-wave schedule, 2 head-ahead (qmha_set_int8_schedule)
-void set_int8_schedule(int mode);
 hipError_t launch_debug_qk_int32(const Int8Workspace& w, int N, int D, int bh, int32_t* S, hipStream_t stream);
 // what the production int8 kernel computed (FL_DUMP instance): S [B*H][N][N] int32 (bias
 // removed), Qi [B*H][N][D] (its in-register Q operand), sQ [B*H][N/32]

@@ -495,41 +495,6 @@ def test_deterministic(dev):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("B,N,dm,h,kind", [
-    (1, 4096, 1024, 16, "normal"),   # one C4 sequence: the call the head-ahead schedule exists for
-    (1, 8192, 1024, 32, "uniform"),  # the reference's own shape (include/config.h:22-28), d = 32
-    (3, 608, 512, 8, "normal"),      # 19 groups: partial workgroup and stage, d = 64
-    (2, 416, 256, 8, "normal"),      # 13 groups, d = 32
-    (1, 64, 128, 2, "normal"),       # two tiles: the shortest pipeline
-    (1, 512, 128, 2, "growing"),     # every tile raises the running max; re-anchors
-])
-def test_int8_head_ahead_bit_identical(dev, B, N, dm, h, kind):
-    """The under-filled-grid schedule (FL_HA: tile head one tile ahead) computes every
-    tile with the same arithmetic and folds the tiles in the same order as the three-wave schedule, so
-    fa_tc_int8_b's output must be bit-identical under qmha_set_int8_schedule(1) and (2); the automatic
-    choice must be one of them."""
-    from quantizedmha_amd import _lib
-    lib = _lib.load()
-    if kind == "growing":
-        rng = np.random.default_rng(7)
-        Q = (rng.standard_normal((B, N, dm)) * 0.2 + 1.0).astype(np.float32)
-        K = ((rng.standard_normal((B, N, dm)) * 0.2 + 1.0) * np.linspace(0.0, 4.0, N, dtype=np.float32)[:, None])
-        K = K.astype(np.float32)
-        V = rng.standard_normal((B, N, dm)).astype(np.float32)
-    else:
-        Q, K, V = rand_inputs(11, B, N, dm, dist=kind)
-    outs = {}
-    try:
-        for mode in (1, 2, 0):
-            assert lib.qmha_set_int8_schedule(mode) >= 0
-            outs[mode] = run("fa_tc_int8_b", Q, K, V, dm, h, dev)
-    finally:
-        lib.qmha_set_int8_schedule(0)
-    assert np.isfinite(outs[1]).all()
-    assert np.array_equal(outs[1], outs[2]), float(np.abs(outs[1] - outs[2]).max())
-    assert np.array_equal(outs[0], outs[1])
-
-
 def test_c_abi_solve_per_variant_libraries(dev, oracle_mod):
     """Bind `solve` from each libqmha_<variant>.so exactly as a reference caller would."""
     N, dm, h = 128, 256, 4

@@ -35,8 +35,6 @@ def main():
                     help="comma-separated subset of batched, async1, solve, batched_again, ref")
     a = ap.parse_args()
     lib = _lib.load()
-    if os.environ.get("QMHA_SCHED"):  # fa_tc_int8_b main-kernel schedule (qmha_set_int8_schedule)
-        lib.qmha_set_int8_schedule(int(os.environ["QMHA_SCHED"]))
     vid = _lib.variant_id(a.variant)
     dev = torch.device("cuda:0")
     B, H, N, d = a.B, a.H, a.N, a.d
