@@ -100,8 +100,7 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //             removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump: the bit-exact
 //             check of the production Q@K^T path; never the production launch)
 //   FL_PT     (pipe kernel) the per-tensor mode fa_tc_int8_pt
-enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576,
-       FL_F16ACC = 4194304 };
+enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576 };
 
 // ---------------------------------------------------------------------------------------
 // One-tile-at-a-time main kernel (every head size; N = 32).
@@ -507,20 +506,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // per-tile head results: score scale c', running max m, Kn, row factor f, sP (with the 2^24 of
     // the f16-subnormal P entries), 1/sP (with f), alpha (PT)
     float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f;
-    // FL_F16ACC (A/B only): P@V accumulates in O across tiles with the tile's
-    // scale inside the P operand, P' = f16(Pi * f16(sP sV 2^(m - anchor) / S)); S = the head's sV
-    // maximum rounded up to a power of two
-    constexpr bool F16ACC = FL & FL_F16ACC;
-    float f16acc_invS = 1.0f, f16acc_S = 1.0f;
-    if constexpr (F16ACC) {
-        float mx = 0.0f;
-        for (int t = lane; t < G; t += 64) mx = fmaxf(mx, svb[t]);
-        mx = wave_max64(mx);
-        const int bits = __float_as_int(mx);
-        const int e = ((bits >> 23) & 255) + ((bits & 0x7FFFFF) ? 1 : 0);
-        f16acc_S = __int_as_float(e << 23);
-        f16acc_invS = __int_as_float((254 - e) << 23);
-    }
     // PT: the score scale sQ * sK * log2(e) / sqrt(d) is one constant per head (KFOLD-rounded once)
     const float c_pt = PT ? __int_as_float((__float_as_int(cq * skb[0]) + 2) & ~3) : 0.0f;
     auto head = [&](const v16i& s, int t) {
@@ -548,7 +533,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
         h_invp = __builtin_amdgcn_rcpf(sp);
         h_invp *= h_f;
-        h_sp = F16ACC ? sp : sp * 16777216.0f;
+        h_sp = sp * 16777216.0f;
     };
 
     issue(0);
@@ -613,7 +598,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                     } else {
                         const int m = op >> 1, ks = op & 1;
                         if (has_prev) {
-                            if constexpr (PT || F16ACC) {  // P@V straight into O
+                            if constexpr (PT) {  // P@V straight into O
                                 o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks], o[m], 0,
                                                                               0, 0);
                             } else {
@@ -632,17 +617,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
         // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
         // overflow it); the pending tile t-1 carries its factor in scale_prev
-        if (!PT && __builtin_amdgcn_ballot_w64(m_new - anchor > (F16ACC ? 8.0f : 48.0f))) {
+        if (!PT && __builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
             const float f = __builtin_amdgcn_exp2f(anchor - m_new);
 #pragma unroll
             for (int m = 0; m < MB; ++m) o[m] *= f;
             l_run *= f;
             scale_prev *= f;
-            if constexpr (F16ACC) {  // the pending tile's P' is in the old anchor's units
-                const _Float16 fh = (_Float16)f;
-                pp[0] *= fh;
-                pp[1] *= fh;
-            }
             anchor = m_new;
         }
         mfmas(0);
@@ -680,29 +660,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // and those low 16 bits are exactly the f16 encoding of Pi * 2^-24; one byte permute
         // packs two entries.  P@V then yields T * 2^-24 exactly (T < 2^20); the O scale
         // carries the 2^24 back.
-        if constexpr (F16ACC) {
-            // t = 1.5*2^23 + 25600 + Pi: its low half is the f16 (1024 + Pi); one packed f16 fma per pair
-            // then gives f16(Pi * c) with one rounding (c = f16(sP sV 2^(m - anchor) / S) per row)
-            const _Float16 ch = (_Float16)(sp * svb[t] * e * f16acc_invS);
-            const _Float16 nch = ch * (_Float16)(-1024.0f);
-            const v2h c2 = {ch, ch}, n2 = {nch, nch};
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE + 25600.0f),
-                            t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE + 25600.0f);
-                v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
-                h2 = h2 * c2 + n2;
-                pc[r >> 2][2 * (r & 3)] = h2[0];
-                pc[r >> 2][2 * (r & 3) + 1] = h2[1];
-            }
-        } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
             const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
             pc[r >> 2][2 * (r & 3)] = h2[0];
             pc[r >> 2][2 * (r & 3) + 1] = h2[1];
-        }
         }
         QMHA_FENCE();
         mfmas(5);
@@ -723,7 +686,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= h_alpha;
             }
-        } else if constexpr (has_prev && !F16ACC) {
+        } else if constexpr (has_prev) {
 #pragma unroll
             for (int m = 0; m < MB; ++m)
 #pragma unroll
@@ -956,12 +919,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
                 for (int m = 0; m < MB; ++m)
                     o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
-        } else if constexpr (F16ACC) {
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int m = 0; m < MB; ++m)
-                    o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
         } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -979,10 +936,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // rescales it exactly to the oracle's O * (sV / 127)
         const float unanchor = PT ? 16777216.0f * (svb[0] / 127.0f) : __builtin_amdgcn_exp2f(anchor - m_run);
         const float l = PT ? half_swap_add(l_run) : half_swap_add(l_run) * unanchor;
-        if constexpr (F16ACC) {
-#pragma unroll
-            for (int m = 0; m < MB; ++m) o[m] *= f16acc_S;
-        }
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
 #pragma unroll
@@ -1141,10 +1094,7 @@ template <int D, int XFL = 0>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream, QkDump dbg = QkDump{}) {
     if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-#ifndef QMHA_AB_F16ACC
-#define QMHA_AB_F16ACC 0
-#endif
-    else if constexpr (D == 64) return fa_int8_pipe_launch<D, 4, kD64Flags | XFL | QMHA_AB_F16ACC>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 64) return fa_int8_pipe_launch<D, 4, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
