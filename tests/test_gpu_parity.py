@@ -154,6 +154,10 @@ def test_int8_pt_full_config_all_heads(dev, oracle_mod):
     assert float(out.min()) >= 0.0 and float(out.max()) <= 1.0
     got, ref = _all_slices_vs_oracle(oracle_mod.fa_int8_pt, Q, K, V, out, d)
     assert_parity("fa_tc_int8_pt", got, ref, N=N)
+    for b in (0, 15):  # one sequence per call (issue-priority fairness on): bit-identical slices
+        one = torch_ext.flash_solve(Q[b], K[b], V[b], H * d, H, kernel="fa_tc_int8_pt")
+        torch.cuda.synchronize()
+        assert torch.equal(one, out[b]), b
 
 
 def test_int8_nan_inputs(dev, oracle_mod):
@@ -589,6 +593,13 @@ def test_full_baseline_config_all_heads(dev, oracle_mod):
     got, ref = _all_slices_vs_oracle(oracle_mod.fa_int8, Q, K, V, out, d)
     assert got.shape == (16, N, 16 * d)
     assert_parity("fa_tc_int8_b", got, ref, N=N)
+    # the reference's calling pattern, one sequence per call: a one-round grid, which the launcher
+    # runs with issue-priority fairness -- scheduling only, so every sequence must
+    # come out bit-identical to its slice of the batched (10.7-round, fairness off) launch
+    for b in (0, 7, 15):
+        one = torch_ext.flash_solve(Q[b], K[b], V[b], H * d, H, kernel="fa_tc_int8_b")
+        torch.cuda.synchronize()
+        assert torch.equal(one, out[b]), b
 
 
 def test_reference_own_config_int8_all_heads(dev, oracle_mod):

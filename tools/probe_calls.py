@@ -35,6 +35,8 @@ def main():
                     help="comma-separated subset of batched, async1, solve, batched_again, ref")
     a = ap.parse_args()
     lib = _lib.load()
+    if os.environ.get("QMHA_OVERLAP"):  # batch chunks with the pre-pass of chunk c+1 beside chunk c's main kernel
+        lib.qmha_set_overlap_chunks(int(os.environ["QMHA_OVERLAP"]))
     vid = _lib.variant_id(a.variant)
     dev = torch.device("cuda:0")
     B, H, N, d = a.B, a.H, a.N, a.d
