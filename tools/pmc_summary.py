@@ -75,6 +75,9 @@ def main():
             d = res[main_k[0]]["derived"]
             if "hbm_read_bytes_per_launch" in d and "hbm_write_bytes_per_launch" in d:
                 j["hbm_bytes_per_launch"] = d["hbm_read_bytes_per_launch"] + d["hbm_write_bytes_per_launch"]
+            for key in ("mfma_busy_pct", "valu_insts_per_wave"):  # bench.py's roofline.mfma_busy_pct
+                if key in d:
+                    j[key] = d[key]
             j["shape"] = a.shape
             j["kernel"] = main_k[0]
         os.makedirs(os.path.dirname(a.json_out), exist_ok=True)
