@@ -389,15 +389,15 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
         g_last_error = "layout 2 (per-tensor scales) is built for d = 32, 64, 128 only";
         return QMHA_ERR_NOSYS;
     }
-    if (layout == 2) {  // per-tensor (head-slice) scales: group absmax pass + quantisation pass
-        const size_t need = qmha::align_up((size_t)3 * B * h * (N / 32) * sizeof(float), 256);
+    if (layout == 2) {  // per-tensor (head-slice) scales: the single-read pass (slice counters in a workspace)
+        const size_t need = qmha::align_up((size_t)6 * B * h * sizeof(uint32_t), 256);
         void* ws = nullptr;
         st = get_workspace(need, (hipStream_t)stream, &ws);
         if (st != QMHA_OK) return st;
         qmha::Int8Workspace w{};
         w.Ki = Xi;  // the K role: int8 rows
         w.sK = scales;
-        w.gmax = static_cast<float*>(ws);
+        w.slice_sync = static_cast<uint32_t*>(ws);
         QMHA_HIP_TRY(qmha::launch_quant_int8_pt_rows(X, w, B, N, h, D, d_model, (hipStream_t)stream), "quant_int8_pt launch");
         return QMHA_OK;
     }

@@ -1047,20 +1047,20 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
 // ---- per-tensor mode (fa_tc_int8_pt) -----------------------------------------------------
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D) {
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t g = align_up((size_t)6 * B * H * sizeof(uint32_t), 256);  // slice_sync [2][3][B*H]
     const size_t s = align_up((size_t)B * H * sizeof(float), 256);
     return e + 2 * e + g + 3 * s;
 }
 
 Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D) {
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t g = align_up((size_t)3 * B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t g = align_up((size_t)6 * B * H * sizeof(uint32_t), 256);  // slice_sync [2][3][B*H]
     const size_t s = align_up((size_t)B * H * sizeof(float), 256);
     char* p = static_cast<char*>(ws);
     Int8Workspace w{};
     w.Ki = reinterpret_cast<int8_t*>(p);
     w.Vh = reinterpret_cast<_Float16*>(p + e);
-    w.gmax = reinterpret_cast<float*>(p + 3 * e);
+    w.slice_sync = reinterpret_cast<uint32_t*>(p + 3 * e);
     w.sQ = reinterpret_cast<float*>(p + 3 * e + g);
     w.sK = reinterpret_cast<float*>(p + 3 * e + g + s);
     w.sV = reinterpret_cast<float*>(p + 3 * e + g + 2 * s);

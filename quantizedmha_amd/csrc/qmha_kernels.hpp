@@ -22,7 +22,7 @@ struct Int8Workspace {
     float* sQ;   // [B*H][N/32]  (per-tensor mode: [B*H], one scale per head slice)
     float* sK;
     float* sV;
-    float* gmax;  // per-tensor mode only: [3][B*H][N/32] group absmax of Q, K, V
+    uint32_t* slice_sync;  // per-tensor mode only: [2][3][B*H] slice absmax bits and part arrivals (qmha_pt_quant_kernel)
 };
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
@@ -33,13 +33,13 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
                              int v_mode, int B, int N, int H, int D, int d_model, hipStream_t stream,
                              int first_tensor = 0, int num_tensors = -1);
 // ---- INT8 per-tensor mode (fa_tc_int8_pt) ----------------------------------------------
-// layout: Ki, Vh as fa_tc_int8_b, then gmax [3][B*H][N/32], then sQ, sK, sV [B*H] each
+// layout: Ki, Vh as fa_tc_int8_b, then slice_sync [2][3][B*H] uint32, then sQ, sK, sV [B*H] each
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D);
-// two launches: group absmax of Q, K, V; K and V quantised with their head-slice scales
+// one pass: K / V quantised with their head-slice scales from registers, sQ (qmha_pt_quant_kernel)
 hipError_t launch_quant_int8_pt(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                 int H, int D, int d_model, hipStream_t stream);
-// the standalone op's per-tensor layout: X in the K role only (absmax pass over X, then int8 rows)
+// the standalone op's per-tensor layout: X in the K role only (int8 rows, one scale per head slice)
 hipError_t launch_quant_int8_pt_rows(const float* X, const Int8Workspace& w, int B, int N, int H, int D, int d_model,
                                      hipStream_t stream);
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,

@@ -33,11 +33,10 @@ namespace qmha {
 // K/V are read exactly once per call.
 // v_mode 0: V as int8 in the i8 V^T operand order (qmha_quantize_int8 layout 1)
 // v_mode 1: V as f16-valued integers in the f16 V^T operand order (main kernel input)
-// slice_sc > 0: per-tensor mode, quantise with that scale (no per-group scale stored)
 template <int D, int VMODE>
 __device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void* __restrict__ Vout,
                                               float* __restrict__ sV, char* vtr, int lane, int b, int k, int g,
-                                              int bh, int N, int G, int d_model, float slice_sc = 0.0f) {
+                                              int bh, int N, int G, int d_model) {
     constexpr int C4 = D / 4, NI = 32 / (64 / C4);
     const int rq = lane / C4, c4 = lane % C4;  // rows NI*rq .. NI*rq+NI-1, columns 4 c4 .. +3
     v4f x[NI];
@@ -49,41 +48,20 @@ __device__ __forceinline__ void quant_v_group(const float* __restrict__ V, void*
 #pragma unroll
         for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[i][c]));
     }
-    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));
+    const float sc = qmha_scale_from_absmax(wave_max64(amax));
     const float inv = 1.0f / sc;
     if constexpr (VMODE == 1)
         vt_group_store<D, true>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(64 * D));
     else
         vt8_group_store<D>(vtr, x, inv, lane, static_cast<char*>(Vout) + ((size_t)bh * G + g) * (size_t)(32 * D));
-    if (lane == 0 && slice_sc == 0.0f) sV[(size_t)bh * G + g] = sc;
-}
-
-// Per-tensor mode (fa_tc_int8_pt): the scale of a head's whole [N, d] slice from the absmax of
-// its G 32-row groups (qmha_group_absmax_kernel): max is exact in any order, so this equals the
-// fp32_to_int8sram arithmetic over the whole slice (fa_tc_int8_b.cu:56-106).  One wave per
-// (tensor, bh) slice reads its G group maxima once and writes the slice scale to s{Q,K,V}[bh]
-// (round-3 ADVICE: every quantising wave used to re-reduce all G maxima of its slice, G^2 reads
-// per slice -- 16 MB per slice and tensor at N = 65536).
-__global__ __launch_bounds__(256) void qmha_slice_scale_kernel(const float* __restrict__ gmax, float* __restrict__ sQ,
-                                                               float* __restrict__ sK, float* __restrict__ sV, int BH,
-                                                               int G, int first_tensor) {
-    const int tensor = blockIdx.y + first_tensor;
-    const int lane = threadIdx.x & 63;
-    const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (bh >= BH) return;  // wave-uniform
-    const float* gm = gmax + ((size_t)tensor * BH + bh) * G;
-    float m = 0.0f;
-    for (int i = lane; i < G; i += 64) m = fmaxf(m, gm[i]);
-    const float sc = qmha_scale_from_absmax(wave_max64(m));
-    float* s_out = tensor == 0 ? sQ : (tensor == 1 ? sK : sV);
-    if (lane == 0 && s_out) s_out[bh] = sc;
+    if (lane == 0) sV[(size_t)bh * G + g] = sc;
 }
 
 // One wave quantises one 32-row group of Q or K (b, k, g) into int8 rows [bh][N][D].
 template <int D>
 __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int8_t* __restrict__ Xi,
                                                 float* __restrict__ sX, int lane, int b, int k, int g, int bh, int N,
-                                                int G, int d_model, float slice_sc = 0.0f) {
+                                                int G, int d_model) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
     const int ri = lane / C4, ci = lane % C4;
     v4f v[NI];
@@ -95,7 +73,7 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
 #pragma unroll
         for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[i][c]));
     }
-    const float sc = slice_sc > 0.0f ? slice_sc : qmha_scale_from_absmax(wave_max64(amax));  // :104
+    const float sc = qmha_scale_from_absmax(wave_max64(amax));  // :104
     const float inv = 1.0f / sc;                                                            // :106 (correctly rounded)
     int8_t* dst = Xi + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
 #pragma unroll
@@ -105,16 +83,14 @@ __device__ __forceinline__ void quant_row_group(const float* __restrict__ X, int
         for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(v[i][c], inv)) << (8 * c);
         *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + ri) * D) = w;
     }
-    if (lane == 0 && slice_sc == 0.0f) sX[(size_t)bh * G + g] = sc;
+    if (lane == 0) sX[(size_t)bh * G + g] = sc;
 }
 
 // ---------------------------------------------------------------------------------------
 // Pre-pass: quantise Q, K, V (fa_tc_int8_b.cu:33-152, fp32_to_int8sram).
 // One wave per (tensor, bh, group); blockIdx.y = tensor (0 Q, 1 K, 2 V).
 // ---------------------------------------------------------------------------------------
-// PT (per-tensor mode): every group of a head slice is quantised with the slice's scale, read from
-// s{K,V}[bh] (qmha_slice_scale_kernel)
-template <int D, int VMODE, bool PT = false>
+template <int D, int VMODE>
 __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
     int8_t* __restrict__ Qi, int8_t* __restrict__ Ki, void* __restrict__ Vout,
@@ -129,44 +105,12 @@ __global__ __launch_bounds__(256) void qmha_quant_int8_kernel(
     const int G = N / QMHA_GROUP;
     const int bh = item / G, g = item % G;
     const int b = bh / H, k = bh % H;
-    float slice_sc = 0.0f;
-    if constexpr (PT) slice_sc = (tensor == 0 ? sQ : (tensor == 1 ? sK : sV))[bh];
     if (tensor == 2)
-        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model, slice_sc);
+        quant_v_group<D, VMODE>(V, Vout, sV, vtr[wave], lane, b, k, g, bh, N, G, d_model);
     else
         quant_row_group<D>(tensor == 0 ? Q : K, tensor == 0 ? Qi : Ki, tensor == 0 ? sQ : sK, lane, b, k, g, bh, N, G,
-                           d_model, slice_sc);
+                           d_model);
 }
-
-// Per-tensor mode, first pass: the absmax of every 32-row group of every head of Q, K and V
-// (blockIdx.y = tensor), one wave per group, gmax = [3][B*H][G].  Reads the three fp32 tensors once.
-template <int D>
-__global__ __launch_bounds__(256) void qmha_group_absmax_kernel(const float* __restrict__ Q, const float* __restrict__ K,
-                                                                const float* __restrict__ V, float* __restrict__ gmax,
-                                                                int N, int H, int d_model, int total_groups,
-                                                                int first_tensor = 0) {
-    constexpr int C4 = D / 4, RPI = 64 / C4, NI = 32 / RPI;
-    const int tensor = blockIdx.y + first_tensor;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int item = blockIdx.x * 4 + wave;
-    if (item >= total_groups) return;  // wave-uniform
-    const int G = N / QMHA_GROUP;
-    const int bh = item / G, g = item % G;
-    const int b = bh / H, k = bh % H;
-    const int ri = lane / C4, ci = lane % C4;
-    const float* X = tensor == 0 ? Q : (tensor == 1 ? K : V);
-    const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-    float amax = 0.0f;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const v4f v = QMHA_PRE_LOAD(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[c]));
-    }
-    amax = wave_max64(amax);
-    if (lane == 0) gmax[(size_t)tensor * total_groups + item] = amax;
-}
-
 
 template <int D>
 __global__ __launch_bounds__(256) void qmha_convert_f16_kernel(
@@ -333,45 +277,221 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
     return hipGetLastError();
 }
 
-// Two launches over the whole batch: the group absmax of Q, K, V, then K / V quantised with their
-// slice scales.  (r03: batch chunks of ~96 MiB of K + V, each absmax pass followed at once by its
-// quantisation so the re-read of K / V could come from the Infinity Cache, measured 0.260 against
-// 0.230 ms at C4, profiles/r03/pt/ab_chunk/)
-// Three launches over the whole batch: the group absmax of Q, K, V (reads the fp32 tensors once),
-// the slice scales, then K / V quantised with them (reads K / V again: 1.54 GB per call at C4, at
-// the HBM roofline).  r03: batch chunks of ~96 MiB of K + V, each absmax pass followed at once by
-// its quantisation so the re-read could come from the Infinity Cache, measured 0.260 against 0.230
-// ms (profiles/r03/pt/ab_chunk/); r04: one workgroup per head slice doing both passes back to back
-// (re-read from the cache) measured 0.270 ms: one workgroup per 1 MiB slice is latency-bound
-// (3.7 TB/s on its 1.0 GB of HBM traffic; profiles/r04/ab_pt_prepass/)
+// ---------------------------------------------------------------------------------------
+// Per-tensor mode, single read (r04): the slice scale needs the absmax of a whole [N, d] head slice
+// before any of its values are quantised.  A slice of K or V is split over `gkv` workgroups; each
+// loads its part (4 waves x PW 32-row groups, 32 KiB per wave) into REGISTERS, reduces it, and
+// publishes the part's absmax to the slice with one agent-scope atomicMax (non-negative float bits
+// order as unsigned ints; max is exact in any order) followed by an atomicAdd on the slice's arrival
+// counter (both returning, so the max is performed before the arrival is).  Lane 0 then polls the
+// counter (agent-scope loads, s_sleep) until all gkv parts have arrived, reads the slice maximum, and
+// the workgroup quantises the data it still holds -- K and V are read from HBM once, not twice.
+// Q needs only its slice scale (the main kernel quantises Q): its parts reduce and publish, and the
+// last part to arrive writes sQ.  Parts of a slice are consecutive workgroups, K / V first; a part
+// waits only for parts dispatched no later than itself.  The wait is bounded: past the bound the
+// workgroup reduces the whole slice itself (the same maximum), so no dispatch order can deadlock it.
+// sync = [2][3][B*H] uint32 (max bits, arrivals), zeroed before the launch.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qmha_zero_u32_kernel(uint32_t* __restrict__ p, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = 0u;
+}
+
+// The part's absmax into the slice maximum, PERFORMED before the caller's arrival increment: a
+// returning atomic and a wait on it (a non-returning global_atomic_umax may still be in flight when
+// the following atomicAdd lands, and a reader that sees all arrivals would then read a maximum short
+// of this part's -- observed as a rare wrong slice scale before this wait was added)
+__device__ __forceinline__ void publish_max(uint32_t* mx, float m) {
+    const uint32_t old = __hip_atomic_fetch_max(mx, __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
+}
+
+// 12-wave workgroups (three waves per SIMD, one workgroup per CU): r04 A/B at C4 (profiles/r04/ab_pt_single_read/)
+// 0.198 ms against 0.206 ms for 4-wave workgroups with the same 32 KiB per wave, 0.204 ms for 48 KiB per wave
+constexpr int kPtWaves = 12;
+__device__ __forceinline__ float wg_max(const float (&pm)[kPtWaves]) {
+    float m = pm[0];
+#pragma unroll
+    for (int i = 1; i < kPtWaves; ++i) m = fmaxf(m, pm[i]);
+    return m;
+}
+// 32-row groups a wave holds in registers: 32 KiB per wave (128 VGPRs of data), 16 KiB at d = 128
+// (its 2-group form spills under the 12-wave register budget)
 template <int D>
-static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
-                                  int H, int d_model, hipStream_t stream) {
+constexpr int pt_groups_per_wave() { return D == 128 ? 1 : 256 / D; }
+
+template <int D>
+__global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int8_t* __restrict__ Ki,
+    _Float16* __restrict__ Vh, float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
+    uint32_t* __restrict__ sync, int N, int H, int d_model, int BH, int gkv, int gq, int kv_first, int kv_tensors,
+    int with_q) {
+    constexpr int C4 = D / 4, NI = D / 8, RPI = 64 / C4;
+    constexpr int PW = pt_groups_per_wave<D>();
+    constexpr int NW = kPtWaves;
+    constexpr int GPB = NW * PW;  // groups per workgroup
+    __shared__ __attribute__((aligned(16))) char vtr[kPtWaves][D * QMHA_VT_PITCH];
+    __shared__ float part_max[kPtWaves];
+    __shared__ float slice_max;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int G = N / QMHA_GROUP;
+    uint32_t* smax = sync;
+    uint32_t* scnt = sync + 3 * BH;
+    // logical item order: per head slice bh its K parts, V parts, Q parts; each XCD takes a contiguous
+    // range of items (xcd_remap), so the parts of a slice are dispatched together by ONE XCD's
+    // dispatcher (consecutive blocks otherwise land on eight different XCDs, which dispatch them
+    // at unrelated times) and every XCD gets the same mix of K / V / Q work
+    const int per_bh = kv_tensors * gkv + (with_q ? gq : 0);
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = item / per_bh, r = item % per_bh;
+    if (r >= kv_tensors * gkv) {  // ---- Q: slice absmax only (workgroup-uniform branch)
+        const int part = r - kv_tensors * gkv;
+        const int b = bh / H, k = bh % H;
+        const int ri = lane / C4, ci = lane % C4;
+        const int per = (G + gq - 1) / gq;
+        float amax = 0.0f;
+        for (int g = part * per + wave; g < min(G, (part + 1) * per); g += NW) {
+            const float* base = Q + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(v[c]));  // IEEE: a NaN is dropped
+            }
+        }
+        amax = wave_max64(amax);
+        if (lane == 0) part_max[wave] = amax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const float m = wg_max(part_max);
+            publish_max(&smax[bh], m);
+            const uint32_t old = atomicAdd(&scnt[bh], 1u);
+            if (old + 1 == (uint32_t)gq)  // the last part: every max is in
+                sQ[bh] = qmha_scale_from_absmax(__uint_as_float(__hip_atomic_load(&smax[bh], __ATOMIC_RELAXED,
+                                                                                   __HIP_MEMORY_SCOPE_AGENT)));
+        }
+        return;
+    }
+    // ---- K / V: part `part` of slice bh of tensor t, held in registers across the wait
+    const int t = kv_first + r / gkv, part = r % gkv;
+    const int b = bh / H, k = bh % H;
+    const bool isv = t == 2;
+    const float* X = isv ? V : K;
+    // K rows: lane (ri, ci) holds rows i * RPI + ri, columns 4 ci..; V: lane (rq, c4) holds NI
+    // consecutive rows of columns 4 c4.. (the vt_group_store map)
+    const int r0 = isv ? (lane / C4) * NI : lane / C4, rs = isv ? 1 : RPI, cc = lane % C4;
+    v4f x[PW][NI];
+    float amax = 0.0f;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int g = part * GPB + wave * PW + j;
+        if (g < G) {
+            const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP + r0) * d_model + (size_t)k * D + 4 * cc;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                x[j][i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * rs) * d_model));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) amax = fmaxf(amax, fabsf(x[j][i][c]));
+            }
+        }
+    }
+    amax = wave_max64(amax);
+    if (lane == 0) part_max[wave] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float m = wg_max(part_max);
+        uint32_t* mx = &smax[(size_t)t * BH + bh];
+        uint32_t* cn = &scnt[(size_t)t * BH + bh];
+        publish_max(mx, m);
+        uint32_t c = atomicAdd(cn, 1u) + 1;
+        // the other parts of this slice are consecutive workgroups dispatched around this one:
+        // normally a few microseconds; bounded at 2 ms of the 100 MHz real-time clock, then the fallback
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (c < (uint32_t)gkv && __builtin_amdgcn_s_memrealtime() - t0 < 200000ull) {
+            __builtin_amdgcn_s_sleep(2);
+            c = __hip_atomic_load(cn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        slice_max = c >= (uint32_t)gkv ? __uint_as_float(__hip_atomic_load(mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                       : -1.0f;
+    }
+    __syncthreads();
+    float sm = slice_max;
+    if (sm < 0.0f) {  // fallback (never taken when the slice's parts are co-resident): reduce the slice here
+        const int ri = lane / C4, ci = lane % C4;
+        float a2 = 0.0f;
+        for (int g = wave; g < G; g += NW) {
+            const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const v4f v = *reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) a2 = fmaxf(a2, fabsf(v[c]));
+            }
+        }
+        a2 = wave_max64(a2);
+        __syncthreads();
+        if (lane == 0) part_max[wave] = a2;
+        __syncthreads();
+        sm = wg_max(part_max);
+    }
+    const float sc = qmha_scale_from_absmax(sm);  // fa_tc_int8_b.cu:104, over the whole slice
+    const float inv = 1.0f / sc;                  // :106 (correctly rounded)
+    if (part == 0 && threadIdx.x == 0) (isv ? sV : sK)[bh] = sc;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int g = part * GPB + wave * PW + j;
+        if (g >= G) continue;  // wave-uniform
+        if (isv) {
+            if (Vh)
+                vt_group_store<D, true>(vtr[wave], x[j], inv, lane,
+                                        reinterpret_cast<char*>(Vh) + ((size_t)bh * G + g) * (size_t)(64 * D));
+        } else {
+            int8_t* dst = Ki + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * cc;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(x[j][i][c], inv)) << (8 * c);
+                *reinterpret_cast<uint32_t*>(dst + (size_t)(i * RPI + r0) * D) = w;
+            }
+        }
+    }
+}
+
+// Per-tensor pre-pass history: r03 ran three launches (group absmax of Q, K, V; slice
+// scales; K / V quantised with them -- reading K / V twice, 1.54 GB per call at C4: 0.230 ms); batch
+// chunks meant to re-read from the Infinity Cache measured 0.260 ms, one workgroup per slice 0.270 ms.
+// r04 ships the single-read kernel above: 1.0 GB per call, 0.198 ms.
+// single-read launch (qmha_pt_quant_kernel): per head slice its K parts, V parts, Q parts (12 waves x
+// pt_groups_per_wave<D>() groups each); the slice counters / maxima zeroed by a kernel of this call
+template <int D>
+static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                                   int H, int d_model, bool rows_only, hipStream_t stream) {
     const int G = N / QMHA_GROUP, BH = B * H;
-    const int total = BH * G;
-    hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 3), dim3(256), 0, stream, Q, K, V, w.gmax, N,
-                       H, d_model, total);
-    hipLaunchKernelGGL(qmha_slice_scale_kernel, dim3((BH + 3) / 4, 3), dim3(256), 0, stream, (const float*)w.gmax, w.sQ,
-                       w.sK, w.sV, BH, G, 0);
-    // K and V quantised with their slice scales (blockIdx.y = tensor - 1); Q by the main kernel
-    hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 2), dim3(256), 0, stream, Q, K, V,
-                       nullptr, w.Ki, (void*)w.Vh, w.sQ, w.sK, w.sV, N, H, d_model, total, 1);
+    constexpr int GPB = kPtWaves * pt_groups_per_wave<D>();
+    const int gkv = (G + GPB - 1) / GPB;
+    uint32_t* sync = w.slice_sync;  // [2][3][BH]
+    // zeroed by a kernel of this call (a kernel node under graph capture; caller scratch is arbitrary)
+    hipLaunchKernelGGL(qmha_zero_u32_kernel, dim3((6 * BH + 255) / 256), dim3(256), 0, stream, sync, 6 * BH);
+    const int kv_tensors = rows_only ? 1 : 2, with_q = rows_only ? 0 : 1;
+    const int grid = kv_tensors * BH * gkv + (with_q ? BH * gkv : 0);
+    hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
+                       rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1, kv_tensors,
+                       with_q);
     return hipGetLastError();
 }
 
 template <int D>
+static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
+                                  int H, int d_model, hipStream_t stream) {
+    return quant_int8_pt1_d<D>(Q, K, V, w, B, N, H, d_model, false, stream);
+}
+
+// the standalone op's per-tensor layout: X in the K role only (int8 rows, sK = the slice scales)
+template <int D>
 static hipError_t quant_int8_pt_rows_d(const float* X, const Int8Workspace& w, int B, int N, int H, int d_model,
                                        hipStream_t stream) {
-    const int G = N / QMHA_GROUP, BH = B * H;
-    const int total = BH * G;
-    // X in the K role (tensor 1) of a [3][B*H][G] gmax table: absmax, slice scales, then int8 rows
-    hipLaunchKernelGGL((qmha_group_absmax_kernel<D>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X, w.gmax, N,
-                       H, d_model, total, 1);
-    hipLaunchKernelGGL(qmha_slice_scale_kernel, dim3((BH + 3) / 4, 1), dim3(256), 0, stream, (const float*)w.gmax, nullptr,
-                       w.sK, nullptr, BH, G, 1);
-    hipLaunchKernelGGL((qmha_quant_int8_kernel<D, 1, true>), dim3((total + 3) / 4, 1), dim3(256), 0, stream, X, X, X,
-                       nullptr, w.Ki, nullptr, nullptr, w.sK, nullptr, N, H, d_model, total, 1);
-    return hipGetLastError();
+    return quant_int8_pt1_d<D>(X, X, X, w, B, N, H, d_model, true, stream);
 }
 
 hipError_t launch_quant_int8_pt_rows(const float* X, const Int8Workspace& w, int B, int N, int H, int D, int d_model,
