@@ -36,6 +36,7 @@
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
+#include <atomic>
 #include <type_traits>
 
 namespace qmha {
@@ -1011,18 +1012,18 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
 // occupancy answer, cached per kernel instance and device); 0 if unknown.
 template <int D, int WAVES, int FL>
 static int pipe_rounds(long long nwg) {
-    static int occ[64] = {}, cus[64] = {};
+    static std::atomic<long long> slots_of[64];  // resident workgroups per device (one word: no torn pair)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (occ[dev] == 0) {
+    long long slots = slots_of[dev].load(std::memory_order_relaxed);
+    if (slots <= 0) {
         int n = 0, c = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, qmha_fa_int8_pipe_kernel<D, WAVES, FL>, WAVES * 64, 0) != hipSuccess ||
             hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0 || c <= 0)
             return 0;
-        cus[dev] = c;
-        occ[dev] = n;
+        slots = (long long)n * c;
+        slots_of[dev].store(slots, std::memory_order_relaxed);
     }
-    const long long slots = (long long)occ[dev] * cus[dev];
     return (int)((nwg + slots - 1) / slots);
 }
 // issue-priority fairness (the kernel's `fair`) for grids of at most this many rounds: measured
