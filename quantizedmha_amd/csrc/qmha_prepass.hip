@@ -306,8 +306,9 @@ __device__ __forceinline__ void publish_max(uint32_t* mx, float m) {
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
 }
 
-// 12-wave workgroups (three waves per SIMD, one workgroup per CU): r04 A/B at C4 (profiles/r04/ab_pt_single_read/)
-// 0.198 ms against 0.206 ms for 4-wave workgroups with the same 32 KiB per wave, 0.204 ms for 48 KiB per wave
+// 12-wave workgroups (three waves per SIMD, one workgroup per CU): r04 A/Bs at C4 (profiles/r04/ab_pt_single_read/)
+// 0.198 ms against 0.206 ms for 4-wave workgroups with the same 32 KiB per wave, 0.204 ms for 48 KiB per
+// wave; 8-wave workgroups 0.198, 6-wave 0.210 against 0.200 ms on another box
 constexpr int kPtWaves = 12;
 __device__ __forceinline__ float wg_max(const float (&pm)[kPtWaves]) {
     float m = pm[0];
