@@ -121,6 +121,10 @@ int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, floa
 /* As qmha_debug_fa_int8_dump for the per-tensor mode (QMHA_FA_TC_INT8_PT): its production schedule
  * plus the stores; Qi is quantised with the head slice's scale, and sQ[B*h][N/32] holds that one
  * scale in every group's entry.  N >= 32.  Device pointers; blocking. */
+/* Test hook: bound, in ticks of the 100 MHz real-time clock, of the per-tensor pre-pass's wait for the
+ * other parts of a head slice (default 200000 = 2 ms; 0 makes every part take its fallback, reducing
+ * the whole slice itself -- the same scale, bit-identical output).  Returns the previous bound. */
+int64_t qmha_debug_set_pt_wait(int64_t ticks);
 int qmha_debug_fa_int8_pt_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                                int h, int32_t *S, int8_t *Qi, float *sQ);
 

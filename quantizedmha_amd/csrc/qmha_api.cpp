@@ -520,6 +520,8 @@ const char* qmha_version(void) { return QMHA_VERSION_STRING; }
 
 const char* qmha_last_error(void) { return g_last_error.c_str(); }
 
+int64_t qmha_debug_set_pt_wait(int64_t ticks) { return qmha::set_pt_wait_ticks(ticks); }
+
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);
     g_overlap_chunks.store(n < 1 ? 1 : (n > 16 ? 16 : n));

@@ -37,6 +37,9 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D);
 // one pass: K / V quantised with their head-slice scales from registers, sQ (qmha_pt_quant_kernel)
+// the per-tensor pre-pass's bounded wait in 100 MHz ticks (default 200000 = 2 ms; 0 forces the
+// fallback); returns the previous value
+long long set_pt_wait_ticks(long long ticks);
 hipError_t launch_quant_int8_pt(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                 int H, int D, int d_model, hipStream_t stream);
 // the standalone op's per-tensor layout: X in the K role only (int8 rows, one scale per head slice)

@@ -5,6 +5,8 @@
 //                           head, sc = max(absmax/127, 1e-8), x_i8 = clamp(rint(x * (1/sc))) --
 //                           K as int8 rows, V as f16-valued integers in the MFMA V^T operand order
 //   qmha_convert_f16_kernel fa_tc_v1a.cu:300-330: K as f16 rows, V in the f16 V^T operand order (RNE)
+#include <atomic>
+
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int8_t* __restrict__ Ki,
     _Float16* __restrict__ Vh, float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
     uint32_t* __restrict__ sync, int N, int H, int d_model, int BH, int gkv, int gq, int kv_first, int kv_tensors,
-    int with_q) {
+    int with_q, unsigned long long wait_ticks) {
     constexpr int C4 = D / 4, NI = D / 8, RPI = 64 / C4;
     constexpr int PW = pt_groups_per_wave<D>();
     constexpr int NW = kPtWaves;
@@ -406,9 +408,10 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
         publish_max(mx, m);
         uint32_t c = atomicAdd(cn, 1u) + 1;
         // the other parts of this slice are consecutive workgroups dispatched around this one:
-        // normally a few microseconds; bounded at 2 ms of the 100 MHz real-time clock, then the fallback
+        // normally a few microseconds; bounded at wait_ticks of the 100 MHz real-time clock (2 ms), then
+        // the fallback (0 forces it: qmha_debug_set_pt_wait, the test of that path)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (c < (uint32_t)gkv && __builtin_amdgcn_s_memrealtime() - t0 < 200000ull) {
+        while (c < (uint32_t)gkv && __builtin_amdgcn_s_memrealtime() - t0 < wait_ticks) {
             __builtin_amdgcn_s_sleep(2);
             c = __hip_atomic_load(cn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -463,6 +466,10 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
 // scales; K / V quantised with them -- reading K / V twice, 1.54 GB per call at C4: 0.230 ms); batch
 // chunks meant to re-read from the Infinity Cache measured 0.260 ms, one workgroup per slice 0.270 ms.
 // r04 ships the single-read kernel above: 1.0 GB per call, 0.198 ms.
+// bounded wait of the parts of a slice, in ticks of the 100 MHz real-time clock (qmha_debug_set_pt_wait)
+static std::atomic<long long> g_pt_wait_ticks{200000};
+long long set_pt_wait_ticks(long long ticks) { return g_pt_wait_ticks.exchange(ticks < 0 ? 0 : ticks); }
+
 // single-read launch (qmha_pt_quant_kernel): per head slice its K parts, V parts, Q parts (12 waves x
 // pt_groups_per_wave<D>() groups each); the slice counters / maxima zeroed by a kernel of this call
 template <int D>
@@ -478,7 +485,7 @@ static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* 
     const int grid = kv_tensors * BH * gkv + (with_q ? BH * gkv : 0);
     hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
                        rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1, kv_tensors,
-                       with_q);
+                       with_q, (unsigned long long)g_pt_wait_ticks.load());
     return hipGetLastError();
 }
 

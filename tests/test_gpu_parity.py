@@ -160,6 +160,31 @@ def test_int8_pt_full_config_all_heads(dev, oracle_mod):
         assert torch.equal(one, out[b]), b
 
 
+@pytest.mark.parametrize("B,N,H,d", [(4, 4096, 16, 64), (2, 1024, 8, 32), (2, 2048, 4, 128), (3, 96, 2, 64)])
+def test_int8_pt_prepass_fallback_bit_identical(dev, B, N, H, d):
+    """The per-tensor pre-pass holds each part of a head slice in registers and waits (bounded) for the
+    slice's other parts; past the bound a part reduces the whole slice itself.  Forcing
+    that fallback for every part (qmha_debug_set_pt_wait(0)) must give the same bytes, scales and output."""
+    from quantizedmha_amd import _lib, torch_ext
+    lib = _lib.load()
+    g = torch.Generator(device=dev).manual_seed(21)
+    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
+    V[0, 5, 3] = 9.0  # a slice-wide outlier: the scale the fallback must find too
+    ref = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_pt")
+    refq = torch_ext.quantize_int8(K, H * d, H, layout=2)
+    torch.cuda.synchronize()
+    prev = lib.qmha_debug_set_pt_wait(0)
+    try:
+        out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_pt")
+        q = torch_ext.quantize_int8(K, H * d, H, layout=2)
+        torch.cuda.synchronize()
+    finally:
+        lib.qmha_debug_set_pt_wait(prev)
+    assert prev == 200000
+    assert torch.equal(out, ref)
+    assert torch.equal(q[0], refq[0]) and torch.equal(q[1], refq[1])
+
+
 def test_int8_nan_inputs(dev, oracle_mod):
     """NaN in the caller's Q / K / V (the pre-passes keep IEEE semantics, round-2 ADVICE; the main
     kernel's in-register Q quantiser zeroes NaNs by an integer test on the bits): the
