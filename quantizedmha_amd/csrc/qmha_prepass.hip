@@ -282,17 +282,17 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
 // ---------------------------------------------------------------------------------------
 // Per-tensor mode, single read (r04): the slice scale needs the absmax of a whole [N, d] head slice
 // before any of its values are quantised.  A slice of K or V is split over `gkv` workgroups; each
-// loads its part (4 waves x PW 32-row groups, 32 KiB per wave) into REGISTERS, reduces it, and
+// loads its part (12 waves x PW 32-row groups, 32 KiB per wave) into REGISTERS, reduces it, and
 // publishes the part's absmax to the slice with one agent-scope atomicMax (non-negative float bits
 // order as unsigned ints; max is exact in any order) followed by an atomicAdd on the slice's arrival
 // counter (both returning, so the max is performed before the arrival is).  Lane 0 then polls the
 // counter (agent-scope loads, s_sleep) until all gkv parts have arrived, reads the slice maximum, and
 // the workgroup quantises the data it still holds -- K and V are read from HBM once, not twice.
 // Q needs only its slice scale (the main kernel quantises Q): its parts reduce and publish, and the
-// last part to arrive writes sQ.  Parts of a slice are consecutive workgroups, K / V first; a part
-// waits only for parts dispatched no later than itself.  The wait is bounded: past the bound the
+// last part to arrive writes sQ.  The parts of a slice are consecutive items of one XCD's block
+// sequence (below), so they are normally resident together.  The wait is bounded: past the bound the
 // workgroup reduces the whole slice itself (the same maximum), so no dispatch order can deadlock it.
-// sync = [2][3][B*H] uint32 (max bits, arrivals), zeroed before the launch.
+// sync = [2][3][B*H] uint32 (max bits, arrivals), zeroed by qmha_zero_u32_kernel in the same call.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void qmha_zero_u32_kernel(uint32_t* __restrict__ p, int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
