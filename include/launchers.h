@@ -125,6 +125,14 @@ int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, floa
  * other parts of a head slice (default 200000 = 2 ms; 0 makes every part take its fallback, reducing
  * the whole slice itself -- the same scale, bit-identical output).  Returns the previous bound. */
 int64_t qmha_debug_set_pt_wait(int64_t ticks);
+/* Test hooks of the fused per-block int8 call (fa_tc_int8_b at d = 32 / 64 / 128, N >= 64: the main
+ * kernel quantises K / V itself).  mode 0 = two launches (pre-pass, then the main
+ * kernel), 1 = fused (default), 2 = fused with every K / V group produced by a workgroup of another
+ * XCD (coherence check); ticks = the bound of a workgroup's wait for its head's groups (100 MHz
+ * clock, default 5000; 0 makes every wave produce its share itself).  All give bit-identical
+ * output.  Each returns the previous value. */
+int qmha_debug_set_int8_fused(int mode);
+int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
 int qmha_debug_fa_int8_pt_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                                int h, int32_t *S, int8_t *Qi, float *sQ);
 

@@ -245,9 +245,16 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
         if (_st != QMHA_OK) return _st;                \
     } while (0)
 
-    if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
+    const int nc0 = (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) ? overlap_chunks(B) : 1;
+    if (variant == QMHA_FA_TC_INT8_B && nc0 == 1 && qmha::int8_fused_on(D, N)) {
+        // one kernel quantises K / V and sweeps (FL_FUSED); its flag zeroing is part of it
+        QMHA_MARK(rec.main, stream, true);
+        QMHA_HIP_TRY(qmha::launch_fa_int8_fused(qmha::int8_carve(ws, B, N, h, D), Q, K, V, O, B, N, h, D, d_model, stream),
+                     "fa_int8 fused launch");
+        QMHA_MARK(rec.main, stream, false);
+    } else if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
         const size_t slab = (size_t)N * d_model;  // floats per sequence
-        const int nc = overlap_chunks(B);
+        const int nc = nc0;
         SideStream* side = nullptr;
         if (nc > 1) {
             int st = get_side(stream, nc, &side);
@@ -521,6 +528,8 @@ const char* qmha_version(void) { return QMHA_VERSION_STRING; }
 const char* qmha_last_error(void) { return g_last_error.c_str(); }
 
 int64_t qmha_debug_set_pt_wait(int64_t ticks) { return qmha::set_pt_wait_ticks(ticks); }
+int qmha_debug_set_int8_fused(int mode) { return qmha::set_int8_fused(mode); }
+int64_t qmha_debug_set_int8_fused_wait(int64_t ticks) { return qmha::set_int8_fused_wait(ticks); }
 
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);

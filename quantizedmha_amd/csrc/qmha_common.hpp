@@ -243,7 +243,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // (tools/lds_banks.py models both sides; the 8-byte read-back stays at its 2-way floor).
 constexpr int QMHA_VT_PITCH = 64 + 8;  // bytes per d-row of the LDS tile (8-byte pad)
 __device__ __forceinline__ int vt_chunk_swz(int d) { return (d >> 4) & 7; }
-template <int D, bool QUANT>
+// COH: the lines are stored as agent-coherent 8-byte stores (sc1: visible to the other XCDs once
+// the wave's stores have completed), for a consumer inside the same launch (the fused int8 kernel)
+template <int D, bool QUANT, bool COH = false>
 __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
     constexpr int C4 = D / 4, NI = D / 8;
     const int rq = lane / C4, c4 = lane % C4;
@@ -268,7 +270,13 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
         const int d = u >> 2, q = u & 3;
         const v2i lo = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q) ^ vt_chunk_swz(d)));
         const v2i hi = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q + 1) ^ vt_chunk_swz(d)));
-        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
+        if constexpr (COH) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(dst + 16 * u);
+            __hip_atomic_store(p, __builtin_bit_cast(uint64_t, lo), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p + 1, __builtin_bit_cast(uint64_t, hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
+        }
     }
 }
 

@@ -101,7 +101,12 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //             removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump: the bit-exact
 //             check of the production Q@K^T path; never the production launch)
 //   FL_PT     (pipe kernel) the per-tensor mode fa_tc_int8_pt
-enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576 };
+//   FL_FUSED  (pipe kernel, per-block mode) the K/V pre-pass done by the kernel's own workgroups
+//             (FusedKV below): one launch per call instead of two
+enum {
+    FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576,
+    FL_FUSED = 2097152
+};
 
 // ---------------------------------------------------------------------------------------
 // One-tile-at-a-time main kernel (every head size; N = 32).
@@ -354,12 +359,135 @@ __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
         if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
 }
 
+// ---------------------------------------------------------------------------------------
+// FL_FUSED (r04): the per-block K/V quantisation (fa_tc_int8_b.cu:33-152, the arithmetic of
+// qmha_prepass.hip quant_row_group / quant_v_group) done by the main kernel's own workgroups, so a
+// call is one launch (plus a flag-zeroing one) and the pre-pass's HBM traffic runs under the
+// VALU-bound sweep instead of before it.
+//
+// Work split.  Workgroup v's "own" groups are the KV groups with the indices of its Q groups
+// (q-block qb: groups 4 qb .. 4 qb + 3 of head v / nqb, one per wave).  The dispatcher deals
+// workgroups to the 8 XCDs round-robin and xcd_remap gives each XCD a contiguous range
+// [c0, c1) of logical ids, dispatched in order; R workgroups of a range are resident at once.
+//   * the first R of a range (the first round) produce their own groups, plus the groups of the
+//     range's first head that belong to the previous range (q-blocks before c0);
+//   * workgroup v produces the own groups of v + R (same range): a round ahead of their consumers.
+// Every workgroup then waits until all G groups of its head are flagged.  A group is always produced
+// by a workgroup dispatched no later than its consumers, so the wait cannot deadlock under in-order
+// dispatch; it is bounded anyway (wait_ticks, s_memrealtime): past the bound a wave produces the
+// missing groups itself (bit-identical bytes, so duplicate producers are harmless).
+// Coherence.  Producers write with agent-coherent (sc1) stores, wait for them (vmcnt(0)), then set
+// the flag; consumers poll the flags with agent-coherent loads.  A consumer's caches hold no line of
+// a group before that group is flagged: the kernel starts with invalidated caches, a group's K / V
+// blocks are whole lines (2 / 4 KiB at d = 64), and the scales are padded to whole 128-byte lines
+// per head (sstride), each read only after the whole head is flagged.
+// ---------------------------------------------------------------------------------------
+struct FusedKV {
+    const float* K;        // the caller's fp32 K, V  [B][N][d_model]
+    const float* V;
+    int8_t* Ki;            // the kernel's K / V / scale arrays (what it streams from)
+    _Float16* Vh;
+    float* sK;             // [B*H][sstride]
+    float* sV;
+    uint32_t* ready;       // [B*H][G]: 1 once group g's Ki, Vh, sK, sV are written (zeroed by the call)
+    int R;                 // resident workgroups per XCD (the launcher's occupancy answer)
+    int sstride;           // scales per head: G rounded up to 32
+    int mode;              // 0 production; 1 test: every group produced by a workgroup of another XCD
+    long long wait_ticks;  // bound of the wait, 100 MHz ticks
+};
+
+// One wave quantises K group g and V group g of head slice bh and publishes them.  NaN inputs are
+// zeroed explicitly (this unit is built with -fno-honor-nans): the IEEE pre-pass's fmaxf drops a NaN
+// from the absmax and __float2int_rn maps it to 0, so the bytes are the same.
+template <int D>
+__device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g, int H, int N, int G, int d_model,
+                                                 int lane, char* T) {
+    constexpr int C4 = D / 4, RPI = 64 / C4, NK = 32 / RPI, NV = D / 8;
+    const int b = bh / H, k = bh % H;
+    const int ri = lane / C4, ci = lane % C4;
+    const size_t base = ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+    v4f kx[NK], vx[NV];
+#pragma unroll
+    for (int i = 0; i < NK; ++i)  // K: rows i * RPI + ri (quant_row_group's map)
+        kx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.K + base + (size_t)(i * RPI + ri) * d_model));
+#pragma unroll
+    for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
+        vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
+    float ka = 0.0f, va = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NK; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            kx[i][c] = nan_to_zero(kx[i][c]);
+            ka = fmaxf(ka, fabsf(kx[i][c]));
+        }
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            vx[i][c] = nan_to_zero(vx[i][c]);
+            va = fmaxf(va, fabsf(vx[i][c]));
+        }
+    const float sk = qmha_scale_from_absmax(wave_max64(ka)), ik = 1.0f / sk;  // :104-106
+    const float sv = qmha_scale_from_absmax(wave_max64(va)), iv = 1.0f / sv;
+    int8_t* kd = f.Ki + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(kx[i][c], ik)) << (8 * c);
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    vt_group_store<D, true, true>(T, vx, iv, lane, reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D));
+    if (lane == 0) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(f.sK) + (size_t)bh * f.sstride + g, __float_as_uint(sk),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(f.sV) + (size_t)bh * f.sstride + g, __float_as_uint(sv),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the group has completed
+    if (lane == 0) __hip_atomic_store(f.ready + (size_t)bh * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until all G groups of head bh are flagged; past the bound, wave `wave` of WAVES produces the
+// missing groups g with g % WAVES == wave itself (every wave of the workgroup does its share).
+template <int D, int WAVES>
+__device__ __forceinline__ void wait_kv_head(const FusedKV& f, int bh, int H, int N, int G, int d_model, int wave, int lane,
+                                          char* T) {
+    const uint32_t* rd = f.ready + (size_t)bh * G;
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool self = false;
+    for (;;) {
+        bool all = true;
+        for (int g0 = 0; g0 < G; g0 += 64) {
+            const int g = g0 + lane;
+            const uint32_t v = g < G ? __hip_atomic_load(rd + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+            uint64_t miss = __builtin_amdgcn_ballot_w64(v != 1u);
+            if (miss) {
+                all = false;
+                if (self)
+                    for (; miss; miss &= miss - 1) {
+                        const int gg = g0 + __builtin_ctzll(miss);
+                        if (gg % WAVES == wave) produce_kv_group<D>(f, bh, gg, H, N, G, d_model, lane, T);
+                    }
+            }
+        }
+        if (all) break;
+        if (!self && __builtin_amdgcn_s_memrealtime() - t0 > f.wait_ticks)
+            self = true;
+        else
+            __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");
+}
+
 template <int D, int WAVES, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
-    const float* __restrict__ sQt = nullptr, int fair = 0) {
+    const float* __restrict__ sQt = nullptr, int fair = 0, FusedKV fz = FusedKV{}) {
     constexpr int SG = 2, RING = 3, PF = RING - 1;  // PF: stages in flight ahead
     constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
     constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
@@ -386,6 +514,53 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // accumulates straight into O (the MFMA C operand); O is rescaled by alpha when a row's
     // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
     constexpr bool PT = FL & FL_PT;
+    constexpr bool FUSED = FL & FL_FUSED;
+    static_assert(!(FUSED && (PT || DUMP)), "FL_FUSED: the per-block production kernel only");
+    if constexpr (FUSED) {
+        // the K / V groups (see FusedKV): each wave's LDS transpose tile sits in the ring, which is
+        // not in use before the first DMA below
+        char* T = reinterpret_cast<char*>(&lds[0][0]) + wave * (D * QMHA_VT_PITCH);
+        static_assert(WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "V^T tiles fit the ring");
+        const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8;
+        auto range_of = [&](int x, int& lo, int& hi) {  // xcd_remap's logical range of XCD x
+            lo = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+            hi = lo + (x < r8 ? q8 + 1 : q8);
+        };
+        int c0, c1;
+        range_of(blockIdx.x % 8, c0, c1);
+        const int pos = wg - c0;
+        // this workgroup's production list: n_own (its own groups, or the test rule's), n_orph (the
+        // range's first head's q-blocks that lie in the previous range), then the groups of workgroup
+        // v_ahead -- before the wait for its own head if a consumer of them may already be waiting
+        int n_own = 0, n_orph = 0, n_pre = 0, n_total = 0, v_own = wg, v_ahead = 0, orph0 = 0, Rp = 1;
+        if (fz.mode == 0) {
+            const int R = fz.R, j0 = c0 % nqb;
+            Rp = min(R, c1 - c0);
+            orph0 = c0 - j0 + pos;  // workgroup ids c0 - j0 + pos + m * Rp < c0
+            v_ahead = wg + R;
+            const bool first = pos < R, ahead = v_ahead < c1;
+            // early: a consumer of those groups is already dispatched (the first round of the range,
+            // or this workgroup's own head when a head is longer than a round)
+            const bool early = ahead && (v_ahead / nqb) * nqb <= (first ? c0 + Rp - 1 : wg);
+            n_own = first ? 1 : 0;
+            n_orph = first && pos < j0 ? (j0 - 1 - pos) / Rp + 1 : 0;
+            n_pre = n_own + n_orph + (early ? 1 : 0);
+            n_total = n_pre + (ahead && !early ? 1 : 0);
+        } else {  // test: workgroup pos of range x produces the own groups of workgroup pos of range x - 1
+            int p0, p1;
+            range_of((blockIdx.x + 7) % 8, p0, p1);
+            v_own = p0 + pos;
+            n_own = n_pre = n_total = v_own < p1 ? 1 : 0;
+        }
+        for (int it = 0;; ++it) {  // wave-uniform; one inlined copy of the producer
+            if (it == n_pre) wait_kv_head<D, WAVES>(fz, bh, H, N, G, d_model, wave, lane, T);
+            if (it >= n_total) break;
+            const int v = it < n_own ? v_own : (it < n_own + n_orph ? orph0 + (it - n_own) * Rp : v_ahead);
+            const int g = (v % nqb) * WAVES + wave;
+            if (g < G) produce_kv_group<D>(fz, v / nqb, g, H, N, G, d_model, lane, T);
+        }
+        __syncthreads();  // every wave is done with its tile before the ring's first DMA
+    }
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
         const float sq = quant_q_operand<D>(qrow, half, qop, PT ? sQt[bh] : 0.0f);
@@ -402,8 +577,15 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     }
     const int8_t* kbase = Ki + (size_t)bh * N * D;
     const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
-    const float* skb = sK + (size_t)bh * (PT ? 1 : G);  // PT: one scale per head slice
-    const float* svb = sV + (size_t)bh * (PT ? 1 : G);
+    const int sstride = PT ? 1 : (FUSED ? fz.sstride : G);  // PT: one scale per head slice
+    // FL_FUSED: these arrays are written by this launch, so their pointers pass through an opaque
+    // asm after the wait (no load through them can move above it), and the scales are then read
+    // through the constant address space (scalar loads, as the two-launch kernel's restrict pointers)
+    using SPtr = std::conditional_t<FUSED, const __attribute__((address_space(4))) float*, const float*>;
+    const float* skg = sK + (size_t)bh * sstride;
+    const float* svg = sV + (size_t)bh * sstride;
+    if constexpr (FUSED) asm volatile("" : "+s"(kbase), "+s"(vbase), "+s"(skg), "+s"(svg));
+    const SPtr skb = (SPtr)skg, svb = (SPtr)svg;
     const int nst = (G + SG - 1) / SG;
 
     // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
@@ -977,23 +1159,30 @@ __global__ __launch_bounds__(64) void qmha_debug_qk_int32_kernel(const int8_t* _
 // ---------------------------------------------------------------------------------------
 // Production layout: Ki, Vh, sK, sV (the main kernel quantises Q in registers).  with_q adds Qi
 // and sQ at the end for the int32 Q@K^T test hook, whose pre-pass quantises Q too.
+// The scale arrays hold [B*H][int8_scale_stride(N)] floats: the fused kernel pads each head's
+// scales to whole 128-byte lines (the two-launch path uses the first B*H*G of them, [B*H][G]).
+// kv_ready: the fused kernel's group flags [B*H][G].
+int int8_scale_stride(int N) { return (int)align_up((size_t)(N / QMHA_GROUP), 32); }
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q) {
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
-    return e + 2 * e + 2 * s + (with_q ? e + s : 0);
+    const size_t s = align_up((size_t)B * H * int8_scale_stride(N) * sizeof(float), 256);
+    const size_t f = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(uint32_t), 256);
+    return e + 2 * e + 2 * s + f + (with_q ? e + s : 0);
 }
 
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
     Int8Workspace w{};
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    const size_t s = align_up((size_t)B * H * int8_scale_stride(N) * sizeof(float), 256);
+    const size_t f = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(uint32_t), 256);
     char* p = static_cast<char*>(ws);
     w.Ki = reinterpret_cast<int8_t*>(p);
     w.Vh = reinterpret_cast<_Float16*>(p + e);
     w.sK = reinterpret_cast<float*>(p + 3 * e);
     w.sV = reinterpret_cast<float*>(p + 3 * e + s);
-    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s) : nullptr;
-    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s) : nullptr;
+    w.kv_ready = reinterpret_cast<uint32_t*>(p + 3 * e + 2 * s);
+    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s + f) : nullptr;
+    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s + f) : nullptr;
     return w;
 }
 
@@ -1011,7 +1200,7 @@ static hipError_t fa_int8_launch(const Int8Workspace& w, const float* Qf, float*
 // Rounds of workgroups a grid of `nwg` takes on this device at the kernel's occupancy (HIP's own
 // occupancy answer, cached per kernel instance and device); 0 if unknown.
 template <int D, int WAVES, int FL>
-static int pipe_rounds(long long nwg) {
+static long long pipe_slots() {
     static std::atomic<long long> slots_of[64];  // resident workgroups per device (one word: no torn pair)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
@@ -1024,7 +1213,12 @@ static int pipe_rounds(long long nwg) {
         slots = (long long)n * c;
         slots_of[dev].store(slots, std::memory_order_relaxed);
     }
-    return (int)((nwg + slots - 1) / slots);
+    return slots;
+}
+template <int D, int WAVES, int FL>
+static int pipe_rounds(long long nwg) {
+    const long long slots = pipe_slots<D, WAVES, FL>();
+    return slots > 0 ? (int)((nwg + slots - 1) / slots) : 0;
 }
 // issue-priority fairness (the kernel's `fair`) for grids of at most this many rounds: measured
 // -3.3 % (one round), -3.7 % (two), -2.4 % (eight, d = 32), and not adopted at C4's 10.7 rounds
@@ -1041,7 +1235,39 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     const int rounds = pipe_rounds<D, WAVES, FL>((long long)B * H * nqb);
     const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)nullptr, fair);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)nullptr, fair, FusedKV{});
+    return hipGetLastError();
+}
+
+// ---- FL_FUSED launch: zero the group flags, then the pipelined kernel that quantises K / V itself
+__global__ __launch_bounds__(256) void qmha_zero_flags_kernel(uint32_t* __restrict__ p, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = 0u;
+}
+static std::atomic<int> g_fused_mode{1};              // 0 off (two launches), 1 on, 2 on with the cross-XCD test rule
+static std::atomic<long long> g_fused_wait{5000};     // 50 us
+int set_int8_fused(int mode) { return g_fused_mode.exchange(mode); }
+long long set_int8_fused_wait(long long ticks) { return g_fused_wait.exchange(ticks); }
+bool int8_fused_on(int D, int N) { return g_fused_mode.load() != 0 && (D == 32 || D == 64 || D == 128) && N / QMHA_GROUP >= 2; }
+
+template <int D, int WAVES, int FL>
+static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O,
+                                       int B, int N, int H, int d_model, hipStream_t stream) {
+    constexpr int FLF = FL | FL_FUSED;
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const long long nwg = (long long)B * H * nqb;
+    const long long slots = pipe_slots<D, WAVES, FLF>();
+    if (slots <= 0 || nwg > INT32_MAX) return hipErrorInvalidValue;
+    const int nflags = B * H * G;
+    hipLaunchKernelGGL(qmha_zero_flags_kernel, dim3((nflags + 255) / 256), dim3(256), 0, stream, w.kv_ready, nflags);
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    const int rounds = (int)((nwg + slots - 1) / slots);
+    const int fair = rounds <= kFairMaxRounds;
+    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, w.kv_ready, (int)(slots / 8 > 0 ? slots / 8 : 1), int8_scale_stride(N),
+               g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load()};
+    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Ki,
+                       w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)nullptr, fair, fz);
     return hipGetLastError();
 }
 
@@ -1077,7 +1303,7 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
     const int rounds = pipe_rounds<D, WAVES, FL | FL_PT>((long long)B * H * nqb);
     const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
-                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ, fair);
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ, fair, FusedKV{});
     return hipGetLastError();
 }
 
@@ -1111,6 +1337,17 @@ hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float
 }
 
 #define QMHA_INT8_D_CASES(X) X(32) X(64) X(96) X(128) X(160) X(192) X(224) X(256)
+
+hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
+                                int N, int H, int D, int d_model, hipStream_t stream) {
+    if (!int8_fused_on(D, N) || !w.kv_ready) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return fa_int8_fused_launch<32, 4, kD32Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_fused_launch<64, 4, kD64Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_fused_launch<128, 4, kD128Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream) {

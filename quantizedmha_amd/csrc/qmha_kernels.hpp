@@ -23,9 +23,21 @@ struct Int8Workspace {
     float* sK;
     float* sV;
     uint32_t* slice_sync;  // per-tensor mode only: [2][3][B*H] slice absmax bits and part arrivals (qmha_pt_quant_kernel)
+    uint32_t* kv_ready;    // per-block fused kernel only: [B*H][N/32] group flags
 };
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
+int int8_scale_stride(int N);  // scales per head in the int8 workspace (N/32 rounded up to 32)
+// The fused per-block call (FL_FUSED): K / V quantised by the main kernel's own workgroups, one
+// launch plus a flag-zeroing one.  int8_fused_on: whether run() takes it (d = 32 / 64 / 128, N >= 64,
+// not switched off); set_int8_fused: 0 off (pre-pass + main), 1 on, 2 on with the test rule that
+// has every group produced on another XCD; set_int8_fused_wait: the wait bound in 100 MHz ticks
+// (0 forces every wave to produce its share of its head itself).  Both return the previous value.
+bool int8_fused_on(int D, int N);
+int set_int8_fused(int mode);
+long long set_int8_fused_wait(long long ticks);
+hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
+                                int N, int H, int D, int d_model, hipStream_t stream);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
 // first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V;
 // num_tensors (default: all from first_tensor on) limits the roles launched (the standalone op)

@@ -163,7 +163,7 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     syms = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
     stubs = set(re.findall(r"__device_stub__(\w+?)ILi(\d+)E(\w*)", syms))
     per = {}
-    dumps = []
+    dumps, fused = [], []
     for name, d, rest in stubs:
         if name.startswith("qmha_gemm"):
             continue
@@ -181,7 +181,15 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
                 rest.replace(f"ELi{f}E", f"ELi{int(f) & ~256}E", 1)
             dumps.append((name, d, twin))
             continue
+        if m and fl == 2 and int(m.group(fl)) & 2097152:  # FL_FUSED: the same schedule plus the K / V production
+            f = m.group(fl)
+            fused.append((name, d, rest.replace(f"ELi{f}E", f"ELi{int(f) & ~2097152}E", 1)))
+            continue
         per.setdefault((name, d), set()).add(rest)
+    # the fused per-block kernel at d = 32 / 64 / 128 is the two-launch schedule with FL_FUSED added
+    assert sorted(d for _, d, _ in fused) == ["128", "32", "64"], fused
+    for name, d, base in fused:
+        assert per[(name, d)] == {base}, (name, d, base)
     # per-block d = 32 / 64 / 128 (pipelined) and 96 / 160 / 192 / 224 / 256 (one-tile kernel),
     # per-tensor d = 32 / 64 / 128
     assert len(dumps) == 11, dumps
