@@ -417,7 +417,10 @@ def main():
     if dry:
         res["dry_run"] = True
     else:
-        res["roofline"] = {"bound": "mfma", "kernel": f"qmha_fa_{'int8' if a.variant == 'fa_tc_int8_b' else a.variant}",
+        kname = f"qmha_fa_{'int8' if a.variant == 'fa_tc_int8_b' else a.variant}"
+        if a.variant == "fa_tc_int8_b" and lib_fused_on(d, N):  # one kernel: K/V quantisation + sweep
+            kname = "qmha_fa_int8_pipe_kernel<FL_FUSED> (K/V quantisation inside; + the flag-zeroing launch)"
+        res["roofline"] = {"bound": "mfma", "kernel": kname,
                            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(achieved / peak, 4), "traffic": traffic,
                            "traffic_source": traffic_src,
@@ -468,6 +471,15 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def lib_fused_on(d, N):
+    """Whether the per-block int8 call runs as one fused kernel (qmha_debug_set_int8_fused reads and
+    restores the library's switch; the default is on for d = 32 / 64 / 128, N >= 64)."""
+    lib = _lib.load()
+    mode = lib.qmha_debug_set_int8_fused(1)
+    lib.qmha_debug_set_int8_fused(mode)
+    return mode != 0 and d in (32, 64, 128) and N >= 64
 
 
 def time_quantize_int8(B, H, N, d, dev, steps=20):

@@ -1259,12 +1259,18 @@ static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, 
     const long long nwg = (long long)B * H * nqb;
     const long long slots = pipe_slots<D, WAVES, FLF>();
     if (slots <= 0 || nwg > INT32_MAX) return hipErrorInvalidValue;
+    const int R = (int)(slots / 8 > 0 ? slots / 8 : 1);
+    if (nqb > R) {  // a head longer than a round of an XCD: the split's producers would run after their
+                    // consumers (tests/test_fused_schedule.py); the two launches instead
+        hipError_t e = launch_quant_int8(Qf, Kf, Vf, w, w.Vh, 1, B, N, H, D, d_model, stream, /*first_tensor=*/1);
+        return e != hipSuccess ? e : fa_int8_pipe_launch<D, WAVES, FL>(w, Qf, O, B, N, H, d_model, stream);
+    }
     const int nflags = B * H * G;
     hipLaunchKernelGGL(qmha_zero_flags_kernel, dim3((nflags + 255) / 256), dim3(256), 0, stream, w.kv_ready, nflags);
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
     const int rounds = (int)((nwg + slots - 1) / slots);
     const int fair = rounds <= kFairMaxRounds;
-    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, w.kv_ready, (int)(slots / 8 > 0 ? slots / 8 : 1), int8_scale_stride(N),
+    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, w.kv_ready, R, int8_scale_stride(N),
                g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load()};
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Ki,
                        w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)nullptr, fair, fz);

@@ -169,7 +169,8 @@ def test_int8_fused_bit_identical(dev, B, N, H, d):
     bit -- with the default work split, with every wave producing its own head after a zero wait
     bound, and (one round, grid % 8 == 0) with every group produced by a workgroup of another XCD.
     Shapes: C4-like, the reference's (2 rounds at d = 32), d = 128, N = 96 (nqb = 1), a ragged grid
-    whose heads straddle the XCD ranges and rounds (B5 H3 N2080), and one long head (nqb > R)."""
+    whose heads straddle the XCD ranges and rounds (B5 H3 N2080), and one head longer than a round
+    (N = 65536: the launcher routes it to the two launches, tests/test_fused_schedule.py)."""
     from quantizedmha_amd import _lib, torch_ext
     lib = _lib.load()
     g = torch.Generator(device=dev).manual_seed(31)
