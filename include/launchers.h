@@ -127,7 +127,7 @@ int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, floa
 int64_t qmha_debug_set_pt_wait(int64_t ticks);
 /* Test hooks of the fused per-block int8 call (fa_tc_int8_b at d = 32 / 64 / 128, N >= 64: the main
  * kernel quantises K / V itself).  mode 0 = two launches (pre-pass, then the main
- * kernel), 1 = fused (default), 2 = fused with every K / V group produced by a workgroup of another
+ * kernel; the default), 1 = fused (opt-in), 2 = fused with every K / V group produced by a workgroup of another
  * XCD (coherence check); ticks = the bound of a workgroup's wait for its head's groups (100 MHz
  * clock, default 5000; 0 makes every wave produce its share itself).  All give bit-identical
  * output.  Each returns the previous value. */

@@ -1244,7 +1244,9 @@ __global__ __launch_bounds__(256) void qmha_zero_flags_kernel(uint32_t* __restri
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[i] = 0u;
 }
-static std::atomic<int> g_fused_mode{1};              // 0 off (two launches), 1 on, 2 on with the cross-XCD test rule
+// 0 two launches (the default: the fused kernel is an opt-in until it has GPU evidence), 1 fused,
+// 2 fused with the cross-XCD test rule
+static std::atomic<int> g_fused_mode{0};
 static std::atomic<long long> g_fused_wait{5000};     // 50 us
 int set_int8_fused(int mode) { return g_fused_mode.exchange(mode); }
 long long set_int8_fused_wait(long long ticks) { return g_fused_wait.exchange(ticks); }

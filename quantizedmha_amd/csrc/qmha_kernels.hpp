@@ -30,7 +30,7 @@ Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = fal
 int int8_scale_stride(int N);  // scales per head in the int8 workspace (N/32 rounded up to 32)
 // The fused per-block call (FL_FUSED): K / V quantised by the main kernel's own workgroups, one
 // launch plus a flag-zeroing one.  int8_fused_on: whether run() takes it (d = 32 / 64 / 128, N >= 64,
-// not switched off); set_int8_fused: 0 off (pre-pass + main), 1 on, 2 on with the test rule that
+// switched on); set_int8_fused: 0 off (pre-pass + main, the default), 1 on, 2 on with the test rule that
 // has every group produced on another XCD; set_int8_fused_wait: the wait bound in 100 MHz ticks
 // (0 forces every wave to produce its share of its head itself).  Both return the previous value.
 bool int8_fused_on(int D, int N);

@@ -4,8 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/r04t; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread \
-    -k "fused" > $O/tests_fused.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_zfused.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests_fused.log 2>&1
 rc=$?; grep -E "passed|failed" $O/tests_fused.log | tail -1; [ $rc -ne 0 ] && { tail -30 $O/tests_fused.log; exit $rc; }
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
     -k "int8 or graph or nan or all_ones or reference or c5 or full_baseline" > $O/tests_int8.log 2>&1

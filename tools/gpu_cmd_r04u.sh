@@ -5,8 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/r04u; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread \
-    -k "fused" > $O/tests_fused.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_zfused.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests_fused.log 2>&1
 rc=$?; grep -E "passed|failed" $O/tests_fused.log | tail -1; [ $rc -ne 0 ] && { tail -40 $O/tests_fused.log; exit $rc; }
 bash tools/gpu_cmd_tests.sh r04u || exit $?
 for r in 1 2; do

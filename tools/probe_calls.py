@@ -37,7 +37,7 @@ def main():
     lib = _lib.load()
     if os.environ.get("QMHA_OVERLAP"):  # batch chunks with the pre-pass of chunk c+1 beside chunk c's main kernel
         lib.qmha_set_overlap_chunks(int(os.environ["QMHA_OVERLAP"]))
-    if os.environ.get("QMHA_FUSED"):  # 0: the int8 pre-pass as its own launch; 1: in the main kernel (default)
+    if os.environ.get("QMHA_FUSED"):  # 0: the int8 pre-pass as its own launch (default); 1: in the main kernel
         lib.qmha_debug_set_int8_fused(int(os.environ["QMHA_FUSED"]))
     vid = _lib.variant_id(a.variant)
     dev = torch.device("cuda:0")
