@@ -121,20 +121,24 @@ int qmha_debug_fa_int8_dump(const float *Q, const float *K, const float *V, floa
 /* As qmha_debug_fa_int8_dump for the per-tensor mode (QMHA_FA_TC_INT8_PT): its production schedule
  * plus the stores; Qi is quantised with the head slice's scale, and sQ[B*h][N/32] holds that one
  * scale in every group's entry.  N >= 32.  Device pointers; blocking. */
-/* Test hook: bound, in ticks of the 100 MHz real-time clock, of the per-tensor pre-pass's wait for the
- * other parts of a head slice (default 200000 = 2 ms; 0 makes every part take its fallback, reducing
- * the whole slice itself -- the same scale, bit-identical output).  Returns the previous bound. */
-int64_t qmha_debug_set_pt_wait(int64_t ticks);
-/* Test hooks of the fused per-block int8 call (fa_tc_int8_b at d = 32 / 64 / 128, N >= 64: the main
- * kernel quantises K / V itself, DESIGN.md 5.2d).  mode 0 = two launches (pre-pass, then the main
- * kernel; the default), 1 = fused (opt-in), 2 = fused with every K / V group produced by a workgroup of another
- * XCD (coherence check); ticks = the bound of a workgroup's wait for its head's groups (100 MHz
- * clock, default 5000; 0 makes every wave produce its share itself).  All give bit-identical
- * output.  Each returns the previous value. */
-int qmha_debug_set_int8_fused(int mode);
-int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
 int qmha_debug_fa_int8_pt_dump(const float *Q, const float *K, const float *V, float *O, int B, int N, int d_model,
                                int h, int32_t *S, int8_t *Qi, float *sQ);
+
+/* Test hook: bound, in ticks of the 100 MHz real-time clock, of the per-tensor pre-pass's wait for the
+ * other parts of a head slice (default 200000 = 2 ms; 0 makes every part take its fallback, reducing
+ * the whole slice itself; negative makes every call take the two-pass form that slices of more parts
+ * than one XCD holds at once always take -- the same scales, bit-identical output).  Returns the
+ * previous bound. */
+int64_t qmha_debug_set_pt_wait(int64_t ticks);
+
+/* Test hooks of the fused per-block int8 call (fa_tc_int8_b at d = 32 / 64 / 128, N >= 64: the main
+ * kernel quantises K / V itself, DESIGN.md 5.2d).  mode 0 = two launches (pre-pass, then the main
+ * kernel), 1 = fused, 2 = fused with every K / V group produced by a workgroup of another XCD
+ * (coherence check); ticks = the bound of a workgroup's wait for its head's groups (100 MHz clock,
+ * default 5000; 0 makes every wave produce its share itself).  All give bit-identical output.  Each
+ * returns the previous value. */
+int qmha_debug_set_int8_fused(int mode);
+int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
 
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);

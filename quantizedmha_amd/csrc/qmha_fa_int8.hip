@@ -1260,10 +1260,11 @@ static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, 
     const int nqb = (G + WAVES - 1) / WAVES;
     const long long nwg = (long long)B * H * nqb;
     const long long slots = pipe_slots<D, WAVES, FLF>();
-    if (slots <= 0 || nwg > INT32_MAX) return hipErrorInvalidValue;
+    if (nwg > INT32_MAX) return hipErrorInvalidValue;
     const int R = (int)(slots / 8 > 0 ? slots / 8 : 1);
-    if (nqb > R) {  // a head longer than a round of an XCD: the split's producers would run after their
-                    // consumers (tests/test_fused_schedule.py); the two launches instead
+    if (slots <= 0 || nqb > R) {  // occupancy unknown, or a head longer than a round of an XCD: the split's
+                                  // producers would run after their consumers (tests/test_fused_schedule.py);
+                                  // the two launches instead
         hipError_t e = launch_quant_int8(Qf, Kf, Vf, w, w.Vh, 1, B, N, H, D, d_model, stream, /*first_tensor=*/1);
         return e != hipSuccess ? e : fa_int8_pipe_launch<D, WAVES, FL>(w, Qf, O, B, N, H, d_model, stream);
     }

@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int8_t* __restrict__ Ki,
     _Float16* __restrict__ Vh, float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
     uint32_t* __restrict__ sync, int N, int H, int d_model, int BH, int gkv, int gq, int kv_first, int kv_tensors,
-    int with_q, unsigned long long wait_ticks) {
+    int with_q, unsigned long long wait_ticks, int phase) {
     constexpr int C4 = D / 4, NI = D / 8, RPI = 64 / C4;
     constexpr int PW = pt_groups_per_wave<D>();
     constexpr int NW = kPtWaves;
@@ -347,14 +347,21 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
     const int per_bh = kv_tensors * gkv + (with_q ? gq : 0);
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = item / per_bh, r = item % per_bh;
-    if (r >= kv_tensors * gkv) {  // ---- Q: slice absmax only (workgroup-uniform branch)
-        const int part = r - kv_tensors * gkv;
+    if (phase == 2 && r >= kv_tensors * gkv) return;  // Q's scale was written by phase 1
+    if (phase == 1 || r >= kv_tensors * gkv) {
+        // ---- slice absmax only (workgroup-uniform branch): Q in every phase; phase 1 (the two-pass form,
+        // for slices of more parts than an XCD holds at once) K and V too, without waiting
+        const bool isq = r >= kv_tensors * gkv;
+        const int tt = isq ? 0 : kv_first + r / gkv;
+        const int part = isq ? r - kv_tensors * gkv : r % gkv;
+        const int np = isq ? gq : gkv;
+        const float* X = tt == 0 ? Q : (tt == 1 ? K : V);
         const int b = bh / H, k = bh % H;
         const int ri = lane / C4, ci = lane % C4;
-        const int per = (G + gq - 1) / gq;
+        const int per = (G + np - 1) / np;
         float amax = 0.0f;
         for (int g = part * per + wave; g < min(G, (part + 1) * per); g += NW) {
-            const float* base = Q + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
+            const float* base = X + ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base + (size_t)(i * RPI + ri) * d_model));
@@ -367,11 +374,13 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
         __syncthreads();
         if (threadIdx.x == 0) {
             const float m = wg_max(part_max);
-            publish_max(&smax[bh], m);
-            const uint32_t old = atomicAdd(&scnt[bh], 1u);
-            if (old + 1 == (uint32_t)gq)  // the last part: every max is in
-                sQ[bh] = qmha_scale_from_absmax(__uint_as_float(__hip_atomic_load(&smax[bh], __ATOMIC_RELAXED,
-                                                                                   __HIP_MEMORY_SCOPE_AGENT)));
+            publish_max(&smax[(size_t)tt * BH + bh], m);
+            if (isq) {
+                const uint32_t old = atomicAdd(&scnt[bh], 1u);
+                if (old + 1 == (uint32_t)gq)  // the last part: every max is in
+                    sQ[bh] = qmha_scale_from_absmax(__uint_as_float(__hip_atomic_load(&smax[bh], __ATOMIC_RELAXED,
+                                                                                       __HIP_MEMORY_SCOPE_AGENT)));
+            }
         }
         return;
     }
@@ -401,7 +410,9 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
     amax = wave_max64(amax);
     if (lane == 0) part_max[wave] = amax;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && phase == 2) {  // the two-pass form: phase 1 (a previous launch) left the maximum
+        slice_max = __uint_as_float(__hip_atomic_load(&smax[(size_t)t * BH + bh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    } else if (threadIdx.x == 0) {
         const float m = wg_max(part_max);
         uint32_t* mx = &smax[(size_t)t * BH + bh];
         uint32_t* cn = &scnt[(size_t)t * BH + bh];
@@ -467,8 +478,28 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
 // chunks meant to re-read from the Infinity Cache measured 0.260 ms, one workgroup per slice 0.270 ms.
 // r04 ships the single-read kernel above: 1.0 GB per call, 0.198 ms.
 // bounded wait of the parts of a slice, in ticks of the 100 MHz real-time clock (qmha_debug_set_pt_wait)
+// (negative: every call takes the two-pass form, the test of that path)
 static std::atomic<long long> g_pt_wait_ticks{200000};
-long long set_pt_wait_ticks(long long ticks) { return g_pt_wait_ticks.exchange(ticks < 0 ? 0 : ticks); }
+long long set_pt_wait_ticks(long long ticks) { return g_pt_wait_ticks.exchange(ticks); }
+
+// workgroups of qmha_pt_quant_kernel<D> one XCD holds at once (HIP's occupancy answer x CUs / 8 XCDs,
+// cached per device); 0 if unknown
+template <int D>
+static int pt_resident_per_xcd() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int r = cache[dev].load(std::memory_order_relaxed);
+    if (r <= 0) {
+        int n = 0, c = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, qmha_pt_quant_kernel<D>, 64 * kPtWaves, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0 || c <= 0)
+            return 0;
+        r = n * c / 8;
+        cache[dev].store(r, std::memory_order_relaxed);
+    }
+    return r;
+}
 
 // single-read launch (qmha_pt_quant_kernel): per head slice its K parts, V parts, Q parts (12 waves x
 // pt_groups_per_wave<D>() groups each); the slice counters / maxima zeroed by a kernel of this call
@@ -483,9 +514,22 @@ static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* 
     hipLaunchKernelGGL(qmha_zero_u32_kernel, dim3((6 * BH + 255) / 256), dim3(256), 0, stream, sync, 6 * BH);
     const int kv_tensors = rows_only ? 1 : 2, with_q = rows_only ? 0 : 1;
     const int grid = kv_tensors * BH * gkv + (with_q ? BH * gkv : 0);
+    // the single read needs every part of a slice resident at once; a slice of more parts than one XCD
+    // holds (d = 128 beyond N = 12288, d = 64 beyond 49152, d = 32 beyond 98304 at one workgroup per CU)
+    // would leave each part waiting out the bound -- those run the two-pass form instead: phase 1 publishes
+    // every part's absmax, phase 2 re-reads K / V and quantises them with the slice maxima (round-4 ADVICE)
+    const int resident = pt_resident_per_xcd<D>();
+    const long long wait_ticks = g_pt_wait_ticks.load();
+    if (resident <= 0 || gkv > resident || wait_ticks < 0) {
+        for (int phase = 1; phase <= 2; ++phase)
+            hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
+                               rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1,
+                               kv_tensors, with_q, 0ull, phase);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
                        rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1, kv_tensors,
-                       with_q, (unsigned long long)g_pt_wait_ticks.load());
+                       with_q, (unsigned long long)wait_ticks, 0);
     return hipGetLastError();
 }
 

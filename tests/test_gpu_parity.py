@@ -178,11 +178,57 @@ def test_int8_pt_prepass_fallback_bit_identical(dev, B, N, H, d):
         out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_pt")
         q = torch_ext.quantize_int8(K, H * d, H, layout=2)
         torch.cuda.synchronize()
+        lib.qmha_debug_set_pt_wait(-1)  # the two-pass form (absmax launch, then quantisation launch)
+        out2 = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_pt")
+        q2 = torch_ext.quantize_int8(K, H * d, H, layout=2)
+        torch.cuda.synchronize()
     finally:
         lib.qmha_debug_set_pt_wait(prev)
     assert prev == 200000
     assert torch.equal(out, ref)
     assert torch.equal(q[0], refq[0]) and torch.equal(q[1], refq[1])
+    assert torch.equal(out2, ref)
+    assert torch.equal(q2[0], refq[0]) and torch.equal(q2[1], refq[1])
+
+
+def test_int8_pt_long_slices_two_pass(dev, oracle_mod):
+    """Head slices of more parts than one XCD holds at once (d = 128, N = 16384: 43 parts of 12 groups per
+    K / V slice against ~32 resident pre-pass workgroups per XCD) take the two-pass pre-pass (round-4 ADVICE:
+    the single read would leave every part waiting out its 2 ms bound).  Checked: the quantised bytes and
+    slice scales bit for bit against the oracle, sampled rows against exact fp64 attention, and a call time
+    far below what one 2 ms wait per part would cost."""
+    import time
+    from quantizedmha_amd import torch_ext
+    N, dm, h = 16384, 256, 2
+    d = dm // h
+    Q, K, V = rand_inputs(77, 1, N, dm)
+    K[9, 3] = 6.0  # slice-wide outlier
+    Xi_ref, sc_ref = oracle_mod.quantize_heads_pt(K[None], dm, h)
+    Xg, scg = torch_ext.quantize_int8(torch.from_numpy(K[None]).to(dev), dm, h, layout=2)
+    assert np.array_equal(scg.cpu().numpy(), sc_ref)
+    assert np.array_equal(Xg.cpu().numpy(), Xi_ref)
+    t = [torch.from_numpy(x).to(dev) for x in (Q, K, V)]
+    out = torch_ext.flash_solve(t[0], t[1], t[2], dm, h, kernel="fa_tc_int8_pt")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        out = torch_ext.flash_solve(t[0], t[1], t[2], dm, h, kernel="fa_tc_int8_pt")
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / 5
+    out = out.cpu().numpy()
+    assert np.isfinite(out).all()
+    rows = np.unique(np.concatenate([np.linspace(0, N - 1, 62).astype(int), [1, N - 2]]))
+    err = 0.0
+    for k in range(h):
+        c = slice(k * d, (k + 1) * d)
+        S = Q[rows, c].astype(np.float64) @ K[:, c].astype(np.float64).T / np.sqrt(d)
+        P = np.exp(S - S.max(axis=1, keepdims=True))
+        ref = (P / P.sum(axis=1, keepdims=True)) @ V[:, c].astype(np.float64)
+        err = max(err, float(np.abs(out[rows, c] - ref).max()))
+    parity_log.record("test_int8_pt_long_slices_two_pass", "fa_tc_int8_pt (vs fp64)", err, 0.0,
+                      TOL_FP64["fa_tc_int8_pt"])
+    assert err <= TOL_FP64["fa_tc_int8_pt"], err
+    assert ms < 20.0, ms  # ~2 ms of compute; 43 parts x 2 ms of waiting would be far above this
 
 
 def test_int8_nan_inputs(dev, oracle_mod):

