@@ -30,9 +30,9 @@
 //      qmha_fa_int8_kernel (also N = 32, where there is nothing to pipeline).
 //
 // This is the production source: only the schedules the library ships.  The r01-r03 experiment
-// branches (ablation perturbations, ring / DMA-split / TSHADOW / ACC1 / FAIR schedules, the
-// per-workgroup timeline) live in tools/ablation/qmha_fa_int8_ablation.hip, which QMHA_ABLATION
-// profiling builds compile instead of this file (tools/build.py).
+// branches (ablation perturbations, ring / DMA-split / TSHADOW / ACC1 schedules, the per-workgroup
+// timeline) were kept in tools/ablation/qmha_fa_int8_ablation.hip until round 5 (git history, up to
+// commit 6d5deec); DESIGN.md cites their measurements.
 #include "qmha_common.hpp"
 #include "qmha_kernels.hpp"
 

@@ -34,3 +34,23 @@ def test_graft_entry_build_from_clean_copy(tmp_path):
         assert (lib / name).is_file(), name
     assert (dst / "quantizedmha_amd" / "bin" / "qmha_profile").is_file()
     assert (dst / "oracle" / "liboracle.so").is_file()
+
+
+@pytest.mark.timeout(600)
+def test_ablation_sources_compile(tmp_path):
+    """The profiling build (QMHA_EXTRA_FLAGS=-DQMHA_ABLATION, tools/build.py) compiles: every source with
+    QMHA_ABLATION-only branches, compile-only, in parallel (round-4 ADVICE: that build had rotted)."""
+    import concurrent.futures as cf
+    csrc = os.path.join(ROOT, "quantizedmha_amd", "csrc")
+    srcs = [n for n in sorted(os.listdir(csrc)) if n.endswith((".hip", ".cpp"))
+            and "QMHA_ABLATION" in open(os.path.join(csrc, n)).read()]
+    assert srcs, "no source has a QMHA_ABLATION branch"
+
+    def compile_one(n):
+        cmd = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DQMHA_ABLATION",
+               "-I", os.path.join(ROOT, "include"), "-I", csrc, "-c", os.path.join(csrc, n), "-o", str(tmp_path / (n + ".o"))]
+        return n, subprocess.run(cmd, capture_output=True, text=True, timeout=580)
+
+    with cf.ThreadPoolExecutor(len(srcs)) as ex:
+        for n, r in ex.map(compile_one, srcs):
+            assert r.returncode == 0, n + ": " + r.stderr[-3000:]

@@ -32,10 +32,11 @@ ARCH = "gfx950"
 
 KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_prepass.hip", "qmha_fa_f32.hip", "qmha_unfused.hip",
                   "qmha_api.cpp"]
-# profiling builds (QMHA_EXTRA_FLAGS=-DQMHA_ABLATION) compile the r01-r03 experiment source of the int8
-# main kernels (ablation perturbations and alternative schedules, d = 32 / 64 / 128 only) in place of
-# the production qmha_fa_int8.hip
-ABLATION_INT8 = os.path.join(ROOT, "tools", "ablation", "qmha_fa_int8_ablation.hip")
+# profiling builds (QMHA_EXTRA_FLAGS=-DQMHA_ABLATION) enable the tuning alternatives of the fp16 / fp32 / api
+# sources.  The r01-r03 int8 experiment source (ablation perturbations, ring / DMA-split / TSHADOW / ACC1
+# schedules, the per-workgroup timeline) was removed in round 5 -- it had fallen behind the production
+# workspace layout and entry points; it is in git history up to commit 6d5deec
+# (tools/ablation/qmha_fa_int8_ablation.hip).  Int8 ablation builds compile the production source.
 VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4, "fa_tc_int8_pt": 5}
 DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
 HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
@@ -45,7 +46,6 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                 "-mllvm", "-amdgpu-mfma-vgpr-form"]
 # profiling builds only, e.g. QMHA_EXTRA_FLAGS=-DQMHA_ABLATION (rebuild with --clean)
 COMMON_FLAGS += os.environ.get("QMHA_EXTRA_FLAGS", "").split()
-ABLATION = "-DQMHA_ABLATION" in COMMON_FLAGS
 if os.environ.get("QMHA_AGPR_FORM"):  # A/B: let MFMA accumulators live in AGPRs
     COMMON_FLAGS = [f for f in COMMON_FLAGS if f not in ("-mllvm", "-amdgpu-mfma-vgpr-form")] + ["-DQMHA_MFMA_AGPR"]
 
@@ -85,7 +85,7 @@ def compile_one(src, extra=()):
     out = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o").replace(".cpp", ".o"))
     if extra:
         out = out.replace(".o", "_" + "_".join(e.strip("-D").replace("=", "") for e in extra) + ".o")
-    full = ABLATION_INT8 if (ABLATION and src == "qmha_fa_int8.hip") else os.path.join(CSRC, src)
+    full = os.path.join(CSRC, src)
     if newer(out, [full] + header_deps() + [__file__]):
         lang = ["-x", "hip"] if src.endswith(".hip") else []
         run([HIPCC] + COMMON_FLAGS + FILE_FLAGS.get(src, []) + list(extra) + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c"] + lang +
