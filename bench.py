@@ -475,7 +475,8 @@ def main():
 
 def lib_fused_on(d, N):
     """Whether the per-block int8 call runs as one fused kernel (qmha_debug_set_int8_fused reads and
-    restores the library's switch; the default is on for d = 32 / 64 / 128, N >= 64)."""
+    restores the library's switch).  The fused form is an opt-in (qmha_debug_set_int8_fused(1)); the
+    library's default is the two launches."""
     lib = _lib.load()
     mode = lib.qmha_debug_set_int8_fused(1)
     lib.qmha_debug_set_int8_fused(mode)

@@ -34,6 +34,7 @@
 // timeline) were kept in tools/ablation/qmha_fa_int8_ablation.hip until round 5 (git history, up to
 // commit 6d5deec); DESIGN.md cites their measurements.
 #include "qmha_common.hpp"
+#include "qmha_fused.hpp"
 #include "qmha_kernels.hpp"
 
 #include <atomic>
@@ -363,24 +364,9 @@ __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
 // FL_FUSED (r04): the per-block K/V quantisation (fa_tc_int8_b.cu:33-152, the arithmetic of
 // qmha_prepass.hip quant_row_group / quant_v_group) done by the main kernel's own workgroups, so a
 // call is one launch (plus a flag-zeroing one) and the pre-pass's HBM traffic runs under the
-// VALU-bound sweep instead of before it.
-//
-// Work split.  Workgroup v's "own" groups are the KV groups with the indices of its Q groups
-// (q-block qb: groups 4 qb .. 4 qb + 3 of head v / nqb, one per wave).  The dispatcher deals
-// workgroups to the 8 XCDs round-robin and xcd_remap gives each XCD a contiguous range
-// [c0, c1) of logical ids, dispatched in order; R workgroups of a range are resident at once.
-//   * the first R of a range (the first round) produce their own groups, plus the groups of the
-//     range's first head that belong to the previous range (q-blocks before c0);
-//   * workgroup v produces the own groups of v + R (same range): a round ahead of their consumers.
-// Every workgroup then waits until all G groups of its head are flagged.  A group is always produced
-// by a workgroup dispatched no later than its consumers, so the wait cannot deadlock under in-order
-// dispatch; it is bounded anyway (wait_ticks, s_memrealtime): past the bound a wave produces the
-// missing groups itself (bit-identical bytes, so duplicate producers are harmless).
-// Coherence.  Producers write with agent-coherent (sc1) stores, wait for them (vmcnt(0)), then set
-// the flag; consumers poll the flags with agent-coherent loads.  A consumer's caches hold no line of
-// a group before that group is flagged: the kernel starts with invalidated caches, a group's K / V
-// blocks are whole lines (2 / 4 KiB at d = 64), and the scales are padded to whole 128-byte lines
-// per head (sstride), each read only after the whole head is flagged.
+// VALU-bound sweep instead of before it.  Work split, flags and coherence: qmha_fused.hpp.  The
+// scales are padded to whole 128-byte lines per head (sstride), each read only after the whole head is
+// flagged.
 // ---------------------------------------------------------------------------------------
 struct FusedKV {
     const float* K;        // the caller's fp32 K, V  [B][N][d_model]
@@ -389,11 +375,8 @@ struct FusedKV {
     _Float16* Vh;
     float* sK;             // [B*H][sstride]
     float* sV;
-    uint32_t* ready;       // [B*H][G]: 1 once group g's Ki, Vh, sK, sV are written (zeroed by the call)
-    int R;                 // resident workgroups per XCD (the launcher's occupancy answer)
     int sstride;           // scales per head: G rounded up to 32
-    int mode;              // 0 production; 1 test: every group produced by a workgroup of another XCD
-    long long wait_ticks;  // bound of the wait, 100 MHz ticks
+    FusedCtl ctl;          // flags, residency, test mode, wait bound
 };
 
 // One wave quantises K group g and V group g of head slice bh and publishes them.  NaN inputs are
@@ -446,40 +429,7 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
         __hip_atomic_store(reinterpret_cast<uint32_t*>(f.sV) + (size_t)bh * f.sstride + g, __float_as_uint(sv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the group has completed
-    if (lane == 0) __hip_atomic_store(f.ready + (size_t)bh * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wait until all G groups of head bh are flagged; past the bound, wave `wave` of WAVES produces the
-// missing groups g with g % WAVES == wave itself (every wave of the workgroup does its share).
-template <int D, int WAVES>
-__device__ __forceinline__ void wait_kv_head(const FusedKV& f, int bh, int H, int N, int G, int d_model, int wave, int lane,
-                                          char* T) {
-    const uint32_t* rd = f.ready + (size_t)bh * G;
-    const long long t0 = __builtin_amdgcn_s_memrealtime();
-    bool self = false;
-    for (;;) {
-        bool all = true;
-        for (int g0 = 0; g0 < G; g0 += 64) {
-            const int g = g0 + lane;
-            const uint32_t v = g < G ? __hip_atomic_load(rd + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
-            uint64_t miss = __builtin_amdgcn_ballot_w64(v != 1u);
-            if (miss) {
-                all = false;
-                if (self)
-                    for (; miss; miss &= miss - 1) {
-                        const int gg = g0 + __builtin_ctzll(miss);
-                        if (gg % WAVES == wave) produce_kv_group<D>(f, bh, gg, H, N, G, d_model, lane, T);
-                    }
-            }
-        }
-        if (all) break;
-        if (!self && __builtin_amdgcn_s_memrealtime() - t0 > f.wait_ticks)
-            self = true;
-        else
-            __builtin_amdgcn_s_sleep(2);
-    }
-    asm volatile("" ::: "memory");
+    fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
 }
 
 template <int D, int WAVES, int FL>
@@ -517,49 +467,13 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     constexpr bool FUSED = FL & FL_FUSED;
     static_assert(!(FUSED && (PT || DUMP)), "FL_FUSED: the per-block production kernel only");
     if constexpr (FUSED) {
-        // the K / V groups (see FusedKV): each wave's LDS transpose tile sits in the ring, which is
-        // not in use before the first DMA below
+        // the K / V groups (qmha_fused.hpp); each wave's LDS transpose tile sits in the ring, which is not
+        // in use before the first DMA below (fused_produce_and_wait ends with a workgroup barrier)
         char* T = reinterpret_cast<char*>(&lds[0][0]) + wave * (D * QMHA_VT_PITCH);
         static_assert(WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "V^T tiles fit the ring");
-        const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8;
-        auto range_of = [&](int x, int& lo, int& hi) {  // xcd_remap's logical range of XCD x
-            lo = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-            hi = lo + (x < r8 ? q8 + 1 : q8);
-        };
-        int c0, c1;
-        range_of(blockIdx.x % 8, c0, c1);
-        const int pos = wg - c0;
-        // this workgroup's production list: n_own (its own groups, or the test rule's), n_orph (the
-        // range's first head's q-blocks that lie in the previous range), then the groups of workgroup
-        // v_ahead -- before the wait for its own head if a consumer of them may already be waiting
-        int n_own = 0, n_orph = 0, n_pre = 0, n_total = 0, v_own = wg, v_ahead = 0, orph0 = 0, Rp = 1;
-        if (fz.mode == 0) {
-            const int R = fz.R, j0 = c0 % nqb;
-            Rp = min(R, c1 - c0);
-            orph0 = c0 - j0 + pos;  // workgroup ids c0 - j0 + pos + m * Rp < c0
-            v_ahead = wg + R;
-            const bool first = pos < R, ahead = v_ahead < c1;
-            // early: a consumer of those groups is already dispatched (the first round of the range,
-            // or this workgroup's own head when a head is longer than a round)
-            const bool early = ahead && (v_ahead / nqb) * nqb <= (first ? c0 + Rp - 1 : wg);
-            n_own = first ? 1 : 0;
-            n_orph = first && pos < j0 ? (j0 - 1 - pos) / Rp + 1 : 0;
-            n_pre = n_own + n_orph + (early ? 1 : 0);
-            n_total = n_pre + (ahead && !early ? 1 : 0);
-        } else {  // test: workgroup pos of range x produces the own groups of workgroup pos of range x - 1
-            int p0, p1;
-            range_of((blockIdx.x + 7) % 8, p0, p1);
-            v_own = p0 + pos;
-            n_own = n_pre = n_total = v_own < p1 ? 1 : 0;
-        }
-        for (int it = 0;; ++it) {  // wave-uniform; one inlined copy of the producer
-            if (it == n_pre) wait_kv_head<D, WAVES>(fz, bh, H, N, G, d_model, wave, lane, T);
-            if (it >= n_total) break;
-            const int v = it < n_own ? v_own : (it < n_own + n_orph ? orph0 + (it - n_own) * Rp : v_ahead);
-            const int g = (v % nqb) * WAVES + wave;
-            if (g < G) produce_kv_group<D>(fz, v / nqb, g, H, N, G, d_model, lane, T);
-        }
-        __syncthreads();  // every wave is done with its tile before the ring's first DMA
+        fused_produce_and_wait<WAVES>(fz.ctl, wg, bh, nqb, G, wave, lane, [&](int pbh, int pg) {
+            produce_kv_group<D>(fz, pbh, pg, H, N, G, d_model, lane, T);
+        });
     }
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
@@ -1273,8 +1187,8 @@ static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, 
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
     const int rounds = (int)((nwg + slots - 1) / slots);
     const int fair = rounds <= kFairMaxRounds;
-    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, w.kv_ready, R, int8_scale_stride(N),
-               g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load()};
+    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, int8_scale_stride(N),
+               FusedCtl{w.kv_ready, R, g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load()}};
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Ki,
                        w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)nullptr, fair, fz);
     return hipGetLastError();

@@ -39,7 +39,7 @@ KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_prepass.hip", "qm
 # (tools/ablation/qmha_fa_int8_ablation.hip).  Int8 ablation builds compile the production source.
 VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4, "fa_tc_int8_pt": 5}
 DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
-HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
+HEADERS = ["qmha_common.hpp", "qmha_fused.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
                 "-Wno-unused-variable", "-Wno-unused-lambda-capture", "-munsafe-fp-atomics",
