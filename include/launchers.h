@@ -139,6 +139,10 @@ int64_t qmha_debug_set_pt_wait(int64_t ticks);
  * returns the previous value. */
 int qmha_debug_set_int8_fused(int mode);
 int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
+/* Measurement hook (results WRONG while nonzero): parts of the fused kernel switched off --
+ * bit 0 the wait for the head's groups, bit 1 the agent-coherent stores and their completion wait, bit 2 all
+ * production, bit 3 the fast quantiser (the exact path for every group).  Returns the previous bits. */
+int qmha_debug_set_int8_fused_ablate(int bits);
 
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);

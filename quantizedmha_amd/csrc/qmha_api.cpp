@@ -530,6 +530,7 @@ const char* qmha_last_error(void) { return g_last_error.c_str(); }
 int64_t qmha_debug_set_pt_wait(int64_t ticks) { return qmha::set_pt_wait_ticks(ticks); }
 int qmha_debug_set_int8_fused(int mode) { return qmha::set_int8_fused(mode); }
 int64_t qmha_debug_set_int8_fused_wait(int64_t ticks) { return qmha::set_int8_fused_wait(ticks); }
+int qmha_debug_set_int8_fused_ablate(int bits) { return qmha::set_int8_fused_ablate(bits); }
 
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);

@@ -245,8 +245,11 @@ constexpr int QMHA_VT_PITCH = 64 + 8;  // bytes per d-row of the LDS tile (8-byt
 __device__ __forceinline__ int vt_chunk_swz(int d) { return (d >> 4) & 7; }
 // COH: the lines are stored as agent-coherent 8-byte stores (sc1: visible to the other XCDs once
 // the wave's stores have completed), for a consumer inside the same launch (the fused int8 kernel)
-template <int D, bool QUANT, bool COH = false>
-__device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
+// The two halves of vt_group_store: vt_tile_write puts hf(a, c) -- this lane's four f16 values of column
+// 4 c4 + c, kv rows NI rq + 4a .. +3 (one 8-byte chunk) -- into the wave's LDS tile; vt_tile_store reads the
+// tile back as 16-byte lines and stores them to dst (a caller may rewrite the tile in between).
+template <int D, class HF>
+__device__ __forceinline__ void vt_tile_write(char* T, int lane, HF&& hf) {
     constexpr int C4 = D / 4, NI = D / 8;
     const int rq = lane / C4, c4 = lane % C4;
 #pragma unroll
@@ -254,14 +257,13 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
         const int d = 4 * c4 + c;
 #pragma unroll
         for (int a = 0; a < NI / 4; ++a) {  // kv rows NI rq + 4a .. +3 -> 4 consecutive slots (one 8-byte chunk)
-            v4h h;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                h[e] = QUANT ? (_Float16)qmha_quant_i8(x[4 * a + e][c], inv) : (_Float16)x[4 * a + e][c];
             const int chunk = slot_of_kv_f16(NI * rq + 4 * a) >> 2;
-            *reinterpret_cast<v4h*>(T + d * QMHA_VT_PITCH + 8 * (chunk ^ vt_chunk_swz(d))) = h;
+            *reinterpret_cast<v4h*>(T + d * QMHA_VT_PITCH + 8 * (chunk ^ vt_chunk_swz(d))) = hf(a, c);
         }
     }
+}
+template <int D, bool COH = false>
+__device__ __forceinline__ void vt_tile_store(const char* T, int lane, char* dst) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     constexpr int LINES = D * 64 / 16;  // 16-byte output lines of the group
@@ -278,6 +280,16 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
             *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
         }
     }
+}
+template <int D, bool QUANT, bool COH = false>
+__device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
+    vt_tile_write<D>(T, lane, [&](int a, int c) {
+        v4h h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = QUANT ? (_Float16)qmha_quant_i8(x[4 * a + e][c], inv) : (_Float16)x[4 * a + e][c];
+        return h;
+    });
+    vt_tile_store<D, COH>(T, lane, dst);
 }
 
 // The same for the int8 V^T operand ([D][32 slots] bytes, kv_of_slot_i8 order; the standalone

@@ -382,6 +382,8 @@ struct FusedKV {
 // One wave quantises K group g and V group g of head slice bh and publishes them.  NaN inputs are
 // zeroed explicitly (this unit is built with -fno-honor-nans): the IEEE pre-pass's fmaxf drops a NaN
 // from the absmax and __float2int_rn maps it to 0, so the bytes are the same.
+// ablate bit 1 (measurements only, qmha_debug_set_int8_fused_ablate): plain stores and no completion wait
+// before the flag.
 template <int D>
 __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g, int H, int N, int G, int d_model,
                                                  int lane, char* T) {
@@ -413,23 +415,34 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
         }
     const float sk = qmha_scale_from_absmax(wave_max64(ka)), ik = 1.0f / sk;  // :104-106
     const float sv = qmha_scale_from_absmax(wave_max64(va)), iv = 1.0f / sv;
+    const bool coh = !(f.ctl.ablate & 2);
     int8_t* kd = f.Ki + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
         uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(kx[i][c], ik)) << (8 * c);
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), w, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t* p = reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D);
+        if (coh)
+            __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            *p = w;
     }
-    vt_group_store<D, true, true>(T, vx, iv, lane, reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D));
+    char* vd = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D);
+    if (coh)
+        vt_group_store<D, true, true>(T, vx, iv, lane, vd);
+    else
+        vt_group_store<D, true, false>(T, vx, iv, lane, vd);
     if (lane == 0) {
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(f.sK) + (size_t)bh * f.sstride + g, __float_as_uint(sk),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(f.sV) + (size_t)bh * f.sstride + g, __float_as_uint(sv),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t* pk = reinterpret_cast<uint32_t*>(f.sK) + (size_t)bh * f.sstride + g;
+        uint32_t* pv = reinterpret_cast<uint32_t*>(f.sV) + (size_t)bh * f.sstride + g;
+        __hip_atomic_store(pk, __float_as_uint(sk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pv, __float_as_uint(sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
+    if (coh)
+        fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
+    else if (lane == 0)
+        __hip_atomic_store(f.ctl.ready + (size_t)bh * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D, int WAVES, int FL>
@@ -506,15 +519,20 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // stage offset rides in soffset, so a stage costs no address arithmetic on the VALU
     constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
     int koff[KJ], voff[VJ];
+    // FL_FUSED: the offsets are computed from a copy of the lane id that an opaque asm makes available only
+    // here, so the compiler cannot hoist them above the K / V production, across which they would be spilled
+    // (and reloaded inside the sweep, each reload a vmcnt(0) wait that drains the LDS-DMA pipeline)
+    int lane_o = lane;
+    if constexpr (FUSED) asm volatile("" : "+v"(lane_o));
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int idx = (wave + jj * WAVES) * 64 + lane_o;
         const int row = idx / (D / 16), cc = swz_src<D>(row, idx % (D / 16));
         koff[jj] = row * D + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int idx = (wave + jj * WAVES) * 64 + lane_o;
         const int grp = idx / (4 * D), w = idx % (4 * D);
         const int d = w >> 2, cv = swz_src<64>(d, w & 3);
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
@@ -1162,7 +1180,9 @@ __global__ __launch_bounds__(256) void qmha_zero_flags_kernel(uint32_t* __restri
 // 2 fused with the cross-XCD test rule
 static std::atomic<int> g_fused_mode{0};
 static std::atomic<long long> g_fused_wait{5000};     // 50 us
+static std::atomic<int> g_fused_ablate{0};            // FusedCtl::ablate (measurements only)
 int set_int8_fused(int mode) { return g_fused_mode.exchange(mode); }
+int set_int8_fused_ablate(int bits) { return g_fused_ablate.exchange(bits); }
 long long set_int8_fused_wait(long long ticks) { return g_fused_wait.exchange(ticks); }
 bool int8_fused_on(int D, int N) { return g_fused_mode.load() != 0 && (D == 32 || D == 64 || D == 128) && N / QMHA_GROUP >= 2; }
 
@@ -1188,7 +1208,7 @@ static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, 
     const int rounds = (int)((nwg + slots - 1) / slots);
     const int fair = rounds <= kFairMaxRounds;
     FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, int8_scale_stride(N),
-               FusedCtl{w.kv_ready, R, g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load()}};
+               FusedCtl{w.kv_ready, R, g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load(), g_fused_ablate.load()}};
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Ki,
                        w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)nullptr, fair, fz);
     return hipGetLastError();

@@ -31,6 +31,9 @@ struct FusedCtl {
     int R;                 // resident workgroups per XCD (the launcher's occupancy answer)
     int mode;              // 0 production; 1 test: every group produced by a workgroup of another XCD
     long long wait_ticks;  // bound of the wait, 100 MHz ticks
+    int ablate;            // measurements only (results wrong): bit 0 no wait for the head's groups; bit 2 no
+                           // production at all (the sweep on whatever the scratch holds); bits 1, 3: the
+                           // producer's (qmha_fa_int8.hip produce_kv_group)
 };
 
 // xcd_remap's logical range [lo, hi) of XCD x for a grid of nwg workgroups
@@ -111,8 +114,9 @@ __device__ __forceinline__ void fused_produce_and_wait(const FusedCtl& f, int wg
         v_own = p0 + pos;
         n_own = n_pre = n_total = v_own < p1 ? 1 : 0;
     }
+    if (f.ablate & 4) n_pre = n_total = 0;
     for (int it = 0;; ++it) {  // wave-uniform; one inlined copy of the producer
-        if (it == n_pre) fused_wait_head<WAVES>(f, bh, G, wave, lane, produce);
+        if (it == n_pre && !(f.ablate & 5)) fused_wait_head<WAVES>(f, bh, G, wave, lane, produce);
         if (it >= n_total) break;
         const int v = it < n_own ? v_own : (it < n_own + n_orph ? orph0 + (it - n_own) * Rp : v_ahead);
         const int g = (v % nqb) * WAVES + wave;

@@ -36,6 +36,7 @@ int int8_scale_stride(int N);  // scales per head in the int8 workspace (N/32 ro
 bool int8_fused_on(int D, int N);
 int set_int8_fused(int mode);
 long long set_int8_fused_wait(long long ticks);
+int set_int8_fused_ablate(int bits);  // FusedCtl::ablate, measurements only
 hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
                                 int N, int H, int D, int d_model, hipStream_t stream);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
