@@ -379,15 +379,24 @@ struct FusedKV {
     FusedCtl ctl;          // flags, residency, test mode, wait bound
 };
 
-// One wave quantises K group g and V group g of head slice bh and publishes them.  NaN inputs are
-// zeroed explicitly (this unit is built with -fno-honor-nans): the IEEE pre-pass's fmaxf drops a NaN
-// from the absmax and __float2int_rn maps it to 0, so the bytes are the same.
-// ablate bit 1 (measurements only, qmha_debug_set_int8_fused_ablate): plain stores and no completion wait
-// before the flag.
+// One wave quantises K group g and V group g of head slice bh and publishes them.
+//   Fast path (r05): absmax by v_max3 on |x|; Pi = rint(RN(x / s)) as the reference's __float2int_rn(x * inv)
+//   -- the product rounded first, then a magic add rounds it half-even to an integer held in the low
+//   bits (u = RN(x * inv) + 1.5 * 2^23, byte 0 of u = the int8), both as packed fp32 ops; K bytes
+//   packed by three v_perm per 4 values; V's f16 integers by one v_cvt_pkrtz per 2 values (exact:
+//   |Pi| <= 128).  No clamp is needed: |x * inv| <= 127 (1 + 2^-22) for finite inputs.  A NaN or an
+//   infinity anywhere in the group shows as a result outside [M - 128, M + 127] (checked by v_max3_u32
+//   on the bits), and that group takes the exact path below instead, before anything is stored.
+//   Exact path (r04; NaN -> 0, this unit is built with -fno-honor-nans): the IEEE pre-pass's fmaxf drops
+//   a NaN from the absmax and __float2int_rn maps it to 0, so the bytes are the same.
+// ablate (DESIGN.md 5.2d measurements only, qmha_debug_set_int8_fused_ablate; bits 0 and 2 in
+// qmha_fused.hpp): bit 1 plain stores and no completion wait before the flag; bit 3 the exact path for
+// every group.
 template <int D>
 __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g, int H, int N, int G, int d_model,
                                                  int lane, char* T) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NK = 32 / RPI, NV = D / 8;
+    constexpr float M = QMHA_MAGIC_RNE;  // 1.5 * 2^23
     const int b = bh / H, k = bh % H;
     const int ri = lane / C4, ci = lane % C4;
     const size_t base = ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
@@ -395,50 +404,123 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
 #pragma unroll
     for (int i = 0; i < NK; ++i)  // K: rows i * RPI + ri (quant_row_group's map)
         kx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.K + base + (size_t)(i * RPI + ri) * d_model));
-#pragma unroll
-    for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
-        vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
-    float ka = 0.0f, va = 0.0f;
-#pragma unroll
-    for (int i = 0; i < NK; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            kx[i][c] = nan_to_zero(kx[i][c]);
-            ka = fmaxf(ka, fabsf(kx[i][c]));
-        }
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            vx[i][c] = nan_to_zero(vx[i][c]);
-            va = fmaxf(va, fabsf(vx[i][c]));
-        }
-    const float sk = qmha_scale_from_absmax(wave_max64(ka)), ik = 1.0f / sk;  // :104-106
-    const float sv = qmha_scale_from_absmax(wave_max64(va)), iv = 1.0f / sv;
     const bool coh = !(f.ctl.ablate & 2);
     int8_t* kd = f.Ki + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-#pragma unroll
-    for (int i = 0; i < NK; ++i) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(kx[i][c], ik)) << (8 * c);
-        uint32_t* p = reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D);
+    char* vd = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D);
+    float* skp = f.sK + (size_t)bh * f.sstride + g;
+    float* svp = f.sV + (size_t)bh * f.sstride + g;
+    auto store_k = [&](uint32_t* p, uint32_t w) {
         if (coh)
             __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
             *p = w;
+    };
+    auto store_scales = [&](float sk, float sv) {
+        if (lane == 0) {
+            store_k(reinterpret_cast<uint32_t*>(skp), __float_as_uint(sk));
+            store_k(reinterpret_cast<uint32_t*>(svp), __float_as_uint(sv));
+        }
+    };
+    const bool allow_fast = !(f.ctl.ablate & 8);
+    // u = RN(x * inv) + M, two at a time (v_pk_mul / v_pk_add, no contraction); hi = the largest bit pattern
+    // the magic constant as an opaque register value of the producer (no CSE with the sweep's own uses)
+    float Mv = M;
+    asm volatile("" : "+v"(Mv));
+    auto q2 = [&](float x0, float x1, float inv, uint32_t& hi) {
+#pragma clang fp contract(off)
+        const v2f u = v2f{x0, x1} * v2f{inv, inv} + v2f{Mv, Mv};
+        hi = max(hi, max(__float_as_uint(u[0]), __float_as_uint(u[1])));
+        return u;
+    };
+    constexpr uint32_t kHi = 0x4B40007Fu;  // bits of M + 127: finite groups stay at or below it
+    // ---- K: int8 rows, stored as they are made; a group with a NaN / infinity is redone exactly (its flag
+    // is set only at the end, so no consumer sees the first bytes)
+    float sk, sv;
+    auto k_exact = [&]() {
+        float ka = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NK; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                kx[i][c] = nan_to_zero(kx[i][c]);
+                ka = fmaxf(ka, fabsf(kx[i][c]));
+            }
+        sk = qmha_scale_from_absmax(wave_max64(ka));
+        const float ik = 1.0f / sk;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(kx[i][c], ik)) << (8 * c);
+            store_k(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), w);
+        }
+    };
+    if (allow_fast) {
+        float ka = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NK; ++i)
+            ka = fmaxf(fmaxf(ka, fmaxf(fabsf(kx[i][0]), fabsf(kx[i][1]))), fmaxf(fabsf(kx[i][2]), fabsf(kx[i][3])));
+        sk = qmha_scale_from_absmax(wave_max64(ka));  // :104-106
+        const float ik = 1.0f / sk;
+        uint32_t hi = 0;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            const v2f u01 = q2(kx[i][0], kx[i][1], ik, hi), u23 = q2(kx[i][2], kx[i][3], ik, hi);
+            const uint32_t t01 = __builtin_amdgcn_perm(__float_as_uint(u01[1]), __float_as_uint(u01[0]), 0x0c0c0400u);
+            const uint32_t t23 = __builtin_amdgcn_perm(__float_as_uint(u23[1]), __float_as_uint(u23[0]), 0x0c0c0400u);
+            store_k(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), __builtin_amdgcn_perm(t23, t01, 0x05040100u));
+        }
+        if (__builtin_amdgcn_ballot_w64(hi > kHi)) k_exact();
+    } else {
+        k_exact();
     }
-    char* vd = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D);
+    // ---- V: f16 integers in the V^T operand order, through the wave's LDS tile (rewritten exactly if needed)
+#pragma unroll
+    for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
+        vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
+    auto v_exact = [&]() {
+        float va = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                vx[i][c] = nan_to_zero(vx[i][c]);
+                va = fmaxf(va, fabsf(vx[i][c]));
+            }
+        sv = qmha_scale_from_absmax(wave_max64(va));
+        const float iv = 1.0f / sv;
+        vt_tile_write<D>(T, lane, [&](int a, int c) {
+            v4h h;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h[e] = (_Float16)qmha_quant_i8(vx[4 * a + e][c], iv);
+            return h;
+        });
+    };
+    if (allow_fast) {
+        float va = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            va = fmaxf(fmaxf(va, fmaxf(fabsf(vx[i][0]), fabsf(vx[i][1]))), fmaxf(fabsf(vx[i][2]), fabsf(vx[i][3])));
+        sv = qmha_scale_from_absmax(wave_max64(va));
+        const float iv = 1.0f / sv;
+        uint32_t hi = 0;
+        vt_tile_write<D>(T, lane, [&](int a, int c) {  // rows 4a .. 4a + 3 of this lane's NV, column c
+            const v2f u01 = q2(vx[4 * a][c], vx[4 * a + 1][c], iv, hi);
+            const v2f u23 = q2(vx[4 * a + 2][c], vx[4 * a + 3][c], iv, hi);
+            const v2f y01 = u01 - v2f{Mv, Mv}, y23 = u23 - v2f{Mv, Mv};  // exact integers
+            const v2h h01 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y01[0], y01[1]));
+            const v2h h23 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y23[0], y23[1]));
+            return v4h{h01[0], h01[1], h23[0], h23[1]};
+        });
+        if (__builtin_amdgcn_ballot_w64(hi > kHi)) v_exact();
+    } else {
+        v_exact();
+    }
     if (coh)
-        vt_group_store<D, true, true>(T, vx, iv, lane, vd);
+        vt_tile_store<D, true>(T, lane, vd);
     else
-        vt_group_store<D, true, false>(T, vx, iv, lane, vd);
-    if (lane == 0) {
-        uint32_t* pk = reinterpret_cast<uint32_t*>(f.sK) + (size_t)bh * f.sstride + g;
-        uint32_t* pv = reinterpret_cast<uint32_t*>(f.sV) + (size_t)bh * f.sstride + g;
-        __hip_atomic_store(pk, __float_as_uint(sk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pv, __float_as_uint(sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        vt_tile_store<D, false>(T, lane, vd);
+    store_scales(sk, sv);
     if (coh)
         fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
     else if (lane == 0)

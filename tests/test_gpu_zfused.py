@@ -135,3 +135,43 @@ def test_int8_default_call_is_fused_and_equals_two_launch(dev):
         lib.qmha_debug_set_int8_fused(prev)
     assert torch.equal(out0, ref0)
     assert not torch.equal(ref0, ref1)
+
+
+@pytest.mark.parametrize("B,N,H,d", [(2, 1024, 8, 64), (1, 512, 4, 32), (2, 512, 2, 128)])
+def test_int8_fused_nan_inf_groups_bit_identical(dev, B, N, H, d):
+    """The fused producer's fast quantiser detects a NaN or an infinity in a K / V group from its magic-biased
+    results and redoes that group exactly (NaN -> 0, an infinity makes the group scale inf and every value 0,
+    as the reference's fp32_to_int8sram).  Groups with NaN / +-inf in K and V, one group all-NaN: the fused call
+    equals the two-launch call bit for bit, on a poisoned caller workspace."""
+    from quantizedmha_amd import _lib
+    lib = _lib.load()
+    vid = _lib.variant_id("fa_tc_int8_b")
+    dm = H * d
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev).manual_seed(5)
+    Q, K, V = (torch.randn(B, N, dm, device=dev, generator=g) for _ in range(3))
+    K[0, 3, 5] = float("nan")
+    K[0, 40, (2 * d + 1) % dm] = float("inf")
+    K.view(torch.int32)[0, 300, 3] = 0x7F800001  # a signalling NaN with a payload
+    V.view(torch.int32)[0, 301, 2] = -0x3FFFFF  # a negative quiet NaN with a payload (0xFFC00001)
+    V[0, 70, 7] = float("nan")
+    V[-1, 100, d + 3] = float("-inf")
+    V[-1, 128:160, 0:d] = float("nan")  # a whole group
+    K[0, 200, 1] = -float("inf")
+    nbytes = lib.qmha_workspace_size(B, N, dm, H, vid)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+
+    def call(fused):
+        O = torch.empty_like(Q)
+        prev = lib.qmha_debug_set_int8_fused(fused)
+        try:
+            ws.random_(0, 256)
+            _lib.check(lib.qmha_solve_ws(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, dm, H, vid,
+                                         ws.data_ptr(), ws.numel(), stream))
+            torch.cuda.synchronize()
+        finally:
+            lib.qmha_debug_set_int8_fused(prev)
+        return O
+
+    ref, out = call(0), call(1)
+    assert torch.equal(torch.nan_to_num(ref, 7.0), torch.nan_to_num(out, 7.0))
