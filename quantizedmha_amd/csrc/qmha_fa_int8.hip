@@ -600,6 +600,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
     // stage offset rides in soffset, so a stage costs no address arithmetic on the VALU
     constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
+    // with at least one wave per piece of a stage, the V pieces go to the waves after the K pieces' (wave vw)
+    constexpr bool SPREAD = WAVES >= KCH / 64 + VCH / 64;
+    const int vw = SPREAD ? (wave + WAVES - KCH / 64) % WAVES : wave;
     int koff[KJ], voff[VJ];
     // FL_FUSED: the offsets are computed from a copy of the lane id that an opaque asm makes available only
     // here, so the compiler cannot hoist them above the K / V production, across which they would be spilled
@@ -614,7 +617,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane_o;
+        const int idx = (vw + jj * WAVES) * 64 + lane_o;
         const int grp = idx / (4 * D), w = idx % (4 * D);
         const int d = w >> 2, cv = swz_src<64>(d, w & 3);
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
@@ -631,7 +634,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         }
 #pragma unroll
         for (int jj = 0; jj < VJ; ++jj) {
-            const int inst = wave + jj * WAVES;
+            const int inst = vw + jj * WAVES;
             if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
                 buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
@@ -1338,6 +1341,9 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
 // with the magic-biased accumulator at a 2-wave budget, 1 wave above d = 128 (O alone is d/2 VGPRs
 // per lane; at 2 waves d = 160 / 192 spill 176 / 372 bytes per lane to scratch).
 constexpr int kD64Flags = FL_MAGIC | FL_KFOLD, kD32Flags = FL_MAGIC | FL_KFOLD;
+#ifndef QMHA_INT8_W64
+#define QMHA_INT8_W64 4  // waves per workgroup of the per-block d = 64 kernel (A/B builds: -DQMHA_INT8_W64=12)
+#endif
 constexpr int kD128Flags = FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2, kPtD32Extra = FL_LB4;
 template <int D>
 constexpr int kAnyFlags = FL_MAGIC | (D > 128 ? FL_LB1 : FL_LB2);
@@ -1346,7 +1352,7 @@ template <int D, int XFL = 0>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream, QkDump dbg = QkDump{}) {
     if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    else if constexpr (D == 64) return fa_int8_pipe_launch<D, 4, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 64) return fa_int8_pipe_launch<D, QMHA_INT8_W64, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
