@@ -143,6 +143,10 @@ int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
  * bit 0 the wait for the head's groups, bit 1 the agent-coherent stores and their completion wait, bit 2 all
  * production, bit 3 the fast quantiser (the exact path for every group).  Returns the previous bits. */
 int qmha_debug_set_int8_fused_ablate(int bits);
+/* Test hook of the fused fp16 call (fa_tc_v1a at d = 32 / 64 / 128: the main kernel converts K / V itself with
+ * the same split and flags).  mode 0 = two launches (the default), 1 = fused, 2 = fused with the
+ * cross-XCD test rule.  Bit-identical output.  Returns the previous mode. */
+int qmha_debug_set_f16_fused(int mode);
 
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);

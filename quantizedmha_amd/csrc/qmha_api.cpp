@@ -252,6 +252,12 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
         QMHA_HIP_TRY(qmha::launch_fa_int8_fused(qmha::int8_carve(ws, B, N, h, D), Q, K, V, O, B, N, h, D, d_model, stream),
                      "fa_int8 fused launch");
         QMHA_MARK(rec.main, stream, false);
+    } else if (variant == QMHA_FA_TC_V1A && nc0 == 1 && qmha::f16_fused_on(D, N)) {
+        // one kernel converts K / V and sweeps (F16_FUSED); its flag zeroing is part of it
+        QMHA_MARK(rec.main, stream, true);
+        QMHA_HIP_TRY(qmha::launch_fa_f16_fused(qmha::f16_carve(ws, B, N, h, D), Q, K, V, O, B, N, h, D, d_model, stream),
+                     "fa_f16 fused launch");
+        QMHA_MARK(rec.main, stream, false);
     } else if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
         const size_t slab = (size_t)N * d_model;  // floats per sequence
         const int nc = nc0;
@@ -531,6 +537,7 @@ int64_t qmha_debug_set_pt_wait(int64_t ticks) { return qmha::set_pt_wait_ticks(t
 int qmha_debug_set_int8_fused(int mode) { return qmha::set_int8_fused(mode); }
 int64_t qmha_debug_set_int8_fused_wait(int64_t ticks) { return qmha::set_int8_fused_wait(ticks); }
 int qmha_debug_set_int8_fused_ablate(int bits) { return qmha::set_int8_fused_ablate(bits); }
+int qmha_debug_set_f16_fused(int mode) { return qmha::set_f16_fused(mode); }
 
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);

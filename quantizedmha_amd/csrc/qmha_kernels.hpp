@@ -81,9 +81,19 @@ struct F16Workspace {
     _Float16* Qh;  // unused (nullptr): the main kernel converts Q in registers
     _Float16* Kh;  // [B*H][N][D]
     _Float16* Vt;  // [B*H][N/32][D][32]  (f16 operand slot order)
+    uint32_t* kv_ready;  // fused kernel only: [B*H][N/32] group flags
 };
 size_t f16_workspace_bytes(int B, int N, int H, int D);
 F16Workspace f16_carve(void* ws, int B, int N, int H, int D);
+// The fused fp16 call (F16_FUSED): K / V converted by the main kernel's own workgroups with
+// the int8 fused kernel's split and flags (qmha_fused.hpp).  f16_fused_on: whether run() takes it
+// (d = 32 / 64 / 128, switched on); set_f16_fused: 0 off (pre-pass + main), 1 on, 2 on with the cross-XCD
+// test rule.  Returns the previous mode.
+bool f16_fused_on(int D, int N);
+int set_f16_fused(int mode);
+hipError_t launch_fa_f16_fused(const F16Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
+                               int N, int H, int D, int d_model, hipStream_t stream);
+hipError_t launch_zero_u32(uint32_t* p, int n, hipStream_t stream);
 hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
                               int H, int D, int d_model, hipStream_t stream);
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,

@@ -298,6 +298,12 @@ __global__ __launch_bounds__(256) void qmha_zero_u32_kernel(uint32_t* __restrict
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[i] = 0u;
 }
+// a kernel, not hipMemsetAsync: under graph capture a memset node did not re-zero on replays
+hipError_t launch_zero_u32(uint32_t* p, int n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(qmha_zero_u32_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, n);
+    return hipGetLastError();
+}
 
 // The part's absmax into the slice maximum, PERFORMED before the caller's arrival increment: a
 // returning atomic and a wait on it (a non-returning global_atomic_umax may still be in flight when

@@ -125,3 +125,17 @@ def test_ranges_match_xcd_remap(nwg):
         c0, c1 = rg[b % 8]
         assert c0 <= img[b] < c1 and img[b] - c0 == b // 8
     assert list(itertools.chain.from_iterable(range(*x) for x in rg)) == list(range(nwg))
+
+
+@pytest.mark.parametrize("B,H,N,R", [
+    (16, 16, 4096, 64),   # C3 at d = 64: 8-wave workgroups (2 per CU x 32 CUs per XCD)
+    (1, 16, 4096, 64),    # one C3 sequence per call
+    (2, 4, 2048, 64),     # d = 128 keeps 4-wave workgroups (checked above); a smaller R here
+    (5, 3, 2080, 48),     # ragged
+    (3, 2, 96, 64),
+])
+def test_fused_split_is_sound_8_wave_workgroups(B, H, N, R):
+    """The same split for the fp16 kernel's 8-wave workgroups (256 query rows, 8 groups produced per workgroup,
+    qmha_fa_f16.hip F16_FUSED)."""
+    late, nwg = check(B, H, N, R, waves=8)
+    assert late == 0, (late, nwg)

@@ -28,8 +28,12 @@ SHAPES = [(2, 1024, 8, 64), (4, 4096, 16, 64), (16, 4096, 16, 64), (1, 8192, 32,
           (2, 2048, 4, 128), (8, 4096, 8, 128), (3, 96, 2, 64), (5, 2080, 3, 64), (1, 65536, 1, 64)]
 
 
-@pytest.mark.parametrize("B,N,H,d", SHAPES)
-def test_int8_fused_bit_identical(dev, B, N, H, d):
+F16_SHAPES = [(2, 1024, 8, 64), (4, 4096, 16, 64), (16, 4096, 16, 64), (1, 8192, 32, 32), (2, 2048, 4, 128),
+              (3, 96, 2, 64), (5, 2080, 3, 64), (1, 65536, 1, 64)]
+
+
+@pytest.mark.parametrize("variant,B,N,H,d", [("fa_tc_int8_b",) + s for s in SHAPES] + [("fa_tc_v1a",) + s for s in F16_SHAPES])
+def test_fused_bit_identical(dev, variant, B, N, H, d):
     """Three input sets X0, X1, X2; references from the two-launch path (mode 0).  Then, with the fused call:
       1. a caller-owned workspace (qmha_solve_ws) filled with random bytes before each call, for each set;
       2. back-to-back calls X0, X1, X2, X0 on that workspace without refilling: each call's scratch holds
@@ -42,10 +46,13 @@ def test_int8_fused_bit_identical(dev, B, N, H, d):
     Shapes: small / one-round / C4 (10.7 rounds) at d = 64, the reference's (2 rounds at d = 32), d = 32 and
     d = 128 one- and multi-round, N = 96 (one q-block), a ragged grid whose heads straddle the XCD ranges and
     rounds (B5 H3 N2080), and one head longer than a round (N = 65536: routed to the two launches,
-    tests/test_fused_schedule.py)."""
+    tests/test_fused_schedule.py).  The fp16 call (fa_tc_v1a, K / V converted inside the sweep with the same
+    split and flags) the same way, without step 4 (its wait bound is fixed)."""
     from quantizedmha_amd import _lib
     lib = _lib.load()
-    vid = _lib.variant_id("fa_tc_int8_b")
+    vid = _lib.variant_id(variant)
+    is8 = variant == "fa_tc_int8_b"
+    set_fused = lib.qmha_debug_set_int8_fused if is8 else lib.qmha_debug_set_f16_fused
     dm = H * d
     stream = torch.cuda.current_stream(dev).cuda_stream
     g = torch.Generator(device=dev).manual_seed(31 + N + B)
@@ -68,7 +75,7 @@ def test_int8_fused_bit_identical(dev, B, N, H, d):
     def poison():
         ws.random_(0, 256, generator=pg)
 
-    prev = lib.qmha_debug_set_int8_fused(0)
+    prev = set_fused(0)
     pw = lib.qmha_debug_set_int8_fused_wait(5000)
     failures = []
 
@@ -82,7 +89,7 @@ def test_int8_fused_bit_identical(dev, B, N, H, d):
         torch.cuda.synchronize()
         for r in refs:
             assert torch.isfinite(r).all()
-        lib.qmha_debug_set_int8_fused(1)
+        set_fused(1)
         for i in range(3):  # 1
             poison()
             expect("poisoned", call(i, ws), i)
@@ -90,16 +97,17 @@ def test_int8_fused_bit_identical(dev, B, N, H, d):
             expect("back-to-back", call(i, ws), i)
         for i in (0, 1):  # 3
             expect("library workspace", call(i), i)
-        lib.qmha_debug_set_int8_fused_wait(0)  # 4
-        poison()
-        expect("forced self-production", call(1, ws), 1)
-        lib.qmha_debug_set_int8_fused_wait(5000)
-        lib.qmha_debug_set_int8_fused(2)  # 5
+        if is8:
+            lib.qmha_debug_set_int8_fused_wait(0)  # 4
+            poison()
+            expect("forced self-production", call(1, ws), 1)
+            lib.qmha_debug_set_int8_fused_wait(5000)
+        set_fused(2)  # 5
         for i in (1, 2):
             poison()
             expect("cross-XCD rule", call(i, ws), i)
     finally:
-        lib.qmha_debug_set_int8_fused(prev)
+        set_fused(prev)
         lib.qmha_debug_set_int8_fused_wait(pw)
     assert pw == 5000
     assert not failures, "; ".join(failures)

@@ -39,6 +39,8 @@ def main():
         lib.qmha_set_overlap_chunks(int(os.environ["QMHA_OVERLAP"]))
     if os.environ.get("QMHA_FUSED"):  # 0: the int8 pre-pass as its own launch (default); 1: in the main kernel
         lib.qmha_debug_set_int8_fused(int(os.environ["QMHA_FUSED"]))
+    if os.environ.get("QMHA_F16_FUSED"):  # fa_tc_v1a: 0 the conversion pre-pass as its own launch, 1 in the main kernel
+        lib.qmha_debug_set_f16_fused(int(os.environ["QMHA_F16_FUSED"]))
     if os.environ.get("QMHA_FUSED_ABLATE"):  # parts of the fused kernel switched off (results wrong: timing only)
         lib.qmha_debug_set_int8_fused_ablate(int(os.environ["QMHA_FUSED_ABLATE"]))
     vid = _lib.variant_id(a.variant)
