@@ -277,7 +277,7 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             QMHA_MARK(rec.pre, pre_s, true);
             if (variant == QMHA_FA_TC_INT8_B) {
                 const qmha::Int8Workspace w = int8_slice(w8, b0, N, h, D);
-                QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, 1, nb, N, h, D,
+                QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, qmha::int8_v_mode(D, N), nb, N, h, D,
                                                      d_model, pre_s, /*first_tensor=*/1), "quant_int8 launch");
             } else {
                 QMHA_HIP_TRY(qmha::launch_convert_f16(Q + b0 * slab, K + b0 * slab, V + b0 * slab, f16_slice(w16, b0, N, h, D),
@@ -466,7 +466,7 @@ int qmha_debug_fa_int8_dump(const float* Q, const float* K, const float* V, floa
     st = get_workspace(need, nullptr, &ws);
     if (st != QMHA_OK) return st;
     const qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
-    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, 1, B, N, h, D, d_model, nullptr, /*first_tensor=*/1),
+    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, qmha::int8_v_mode(D, N), B, N, h, D, d_model, nullptr, /*first_tensor=*/1),
                  "quant_int8 launch");
     QMHA_HIP_TRY(qmha::launch_fa_int8_dump(w, Q, O, B, N, h, D, d_model, qmha::QkDump{S, Qi, sQ}, nullptr),
                  "fa_int8 dump launch");

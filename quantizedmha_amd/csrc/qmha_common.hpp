@@ -296,7 +296,8 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
 // qmha_quantize_int8 layout 1): four consecutive kv rows are four consecutive slots, so a lane
 // packs its 4-row runs of one column into one dword (ds_write_b32 instead of byte stores).
 constexpr int QMHA_VT8_PITCH = 32 + 4;  // bytes per d-row of the int8 LDS tile
-template <int D>
+// COH: agent-coherent 8-byte stores (the fused int8 kernel's producers under FL_I8PV)
+template <int D, bool COH = false>
 __device__ __forceinline__ void vt8_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
     constexpr int C4 = D / 4, NI = D / 8;
     const int rq = lane / C4, c4 = lane % C4;
@@ -318,6 +319,12 @@ __device__ __forceinline__ void vt8_group_store(char* T, const v4f (&x)[D / 8], 
     for (int u = lane; u < LINES; u += 64) {
         const int d = u >> 1, q = u & 1;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(T + d * QMHA_VT8_PITCH + 16 * q);
-        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{(int)r[0], (int)r[1], (int)r[2], (int)r[3]};
+        if constexpr (COH) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(dst + 16 * u);
+            __hip_atomic_store(p, (uint64_t)r[0] | ((uint64_t)r[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p + 1, (uint64_t)r[2] | ((uint64_t)r[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{(int)r[0], (int)r[1], (int)r[2], (int)r[3]};
+        }
     }
 }

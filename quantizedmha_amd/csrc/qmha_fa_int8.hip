@@ -104,9 +104,12 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //   FL_PT     (pipe kernel) the per-tensor mode fa_tc_int8_pt
 //   FL_FUSED  (pipe kernel, per-block mode) the K/V pre-pass done by the kernel's own workgroups
 //             (FusedKV below): one launch per call instead of two
+//   FL_I8PV   (pipe kernel, per-block mode) P@V on v_mfma_i32_32x32x32_i8: V staged as int8 in the i8
+//             V^T operand order (half the bytes), P packed to bytes, the int32 result read off its
+//             magic-biased accumulator; bit-identical to the f16 form (see the kernel)
 enum {
     FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576,
-    FL_FUSED = 2097152
+    FL_FUSED = 2097152, FL_I8PV = 4194304
 };
 
 // ---------------------------------------------------------------------------------------
@@ -392,7 +395,7 @@ struct FusedKV {
 // ablate (DESIGN.md 5.2d measurements only, qmha_debug_set_int8_fused_ablate; bits 0 and 2 in
 // qmha_fused.hpp): bit 1 plain stores and no completion wait before the flag; bit 3 the exact path for
 // every group.
-template <int D>
+template <int D, bool V8 = false>  // V8: V as int8 in the i8 V^T operand order (FL_I8PV), exact quantiser
 __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g, int H, int N, int G, int d_model,
                                                  int lane, char* T) {
     constexpr int C4 = D / 4, RPI = 64 / C4, NK = 32 / RPI, NV = D / 8;
@@ -475,6 +478,25 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
         k_exact();
     }
     // ---- V: f16 integers in the V^T operand order, through the wave's LDS tile (rewritten exactly if needed)
+    if constexpr (V8) {  // FL_I8PV: int8 V^T, the pre-pass's exact arithmetic (quant_v_group, v_mode 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt8_group_store's map)
+            vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
+        float va = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                vx[i][c] = nan_to_zero(vx[i][c]);
+                va = fmaxf(va, fabsf(vx[i][c]));
+            }
+        sv = qmha_scale_from_absmax(wave_max64(va));
+        char* vd8 = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(32 * D);
+        if (coh)
+            vt8_group_store<D, true>(T, vx, 1.0f / sv, lane, vd8);
+        else
+            vt8_group_store<D, false>(T, vx, 1.0f / sv, lane, vd8);
+    } else {
 #pragma unroll
     for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
         vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
@@ -520,6 +542,7 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
         vt_tile_store<D, true>(T, lane, vd);
     else
         vt_tile_store<D, false>(T, lane, vd);
+    }
     store_scales(sk, sv);
     if (coh)
         fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
@@ -534,8 +557,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
     const float* __restrict__ sQt = nullptr, int fair = 0, FusedKV fz = FusedKV{}) {
     constexpr int SG = 2, RING = 3, PF = RING - 1;  // PF: stages in flight ahead
-    constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
-    constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
+    constexpr bool I8PV = FL & FL_I8PV;
+    constexpr int KBYTES = SG * 32 * D;                    // K int8 per stage
+    constexpr int VBYTES = SG * 32 * D * (I8PV ? 1 : 2);  // V int8 (FL_I8PV) or f16 per stage
     constexpr int SBYTES = KBYTES + VBYTES;
     constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
     constexpr bool MAGIC = FL & FL_MAGIC;
@@ -561,13 +585,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     constexpr bool PT = FL & FL_PT;
     constexpr bool FUSED = FL & FL_FUSED;
     static_assert(!(FUSED && (PT || DUMP)), "FL_FUSED: the per-block production kernel only");
+    static_assert(!(I8PV && PT), "FL_I8PV: the per-block contract (the per-tensor P@V accumulates across tiles)");
     if constexpr (FUSED) {
         // the K / V groups (qmha_fused.hpp); each wave's LDS transpose tile sits in the ring, which is not
         // in use before the first DMA below (fused_produce_and_wait ends with a workgroup barrier)
         char* T = reinterpret_cast<char*>(&lds[0][0]) + wave * (D * QMHA_VT_PITCH);
         static_assert(WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "V^T tiles fit the ring");
         fused_produce_and_wait<WAVES>(fz.ctl, wg, bh, nqb, G, wave, lane, [&](int pbh, int pg) {
-            produce_kv_group<D>(fz, pbh, pg, H, N, G, d_model, lane, T);
+            produce_kv_group<D, I8PV>(fz, pbh, pg, H, N, G, d_model, lane, T);
         });
     }
     if (active) {
@@ -585,7 +610,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         for (int ks = 0; ks < D / 32; ++ks) qop[ks] = v4i{0, 0, 0, 0};
     }
     const int8_t* kbase = Ki + (size_t)bh * N * D;
-    const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
+    const char* vbase = reinterpret_cast<const char*>(Vh) + (size_t)bh * N * D * (I8PV ? 1 : 2);
     const int sstride = PT ? 1 : (FUSED ? fz.sstride : G);  // PT: one scale per head slice
     // FL_FUSED: these arrays are written by this launch, so their pointers pass through an opaque
     // asm after the wait (no load through them can move above it), and the scales are then read
@@ -618,9 +643,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
         const int idx = (vw + jj * WAVES) * 64 + lane_o;
-        const int grp = idx / (4 * D), w = idx % (4 * D);
-        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
-        voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
+        if constexpr (I8PV) {  // 32-byte V^T rows (32 keys of one d), two 16-byte chunks each
+            const int r = idx >> 1, grp = r / D, d = r % D;
+            voff[jj] = grp * 32 * D + d * 32 + 16 * swz_src<32>(d, idx & 1);
+        } else {
+            const int grp = idx / (4 * D), w = idx % (4 * D);
+            const int d = w >> 2, cv = swz_src<64>(d, w & 3);
+            voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
+        }
     }
     // stage st into ring slot `slot` (= st % RING; a compile-time constant in the unrolled loop)
     auto issue_at = [&](int st, int slot) {
@@ -636,7 +666,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         for (int jj = 0; jj < VJ; ++jj) {
             const int inst = vw + jj * WAVES;
             if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
-                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
+                buffer_load_lds16(vbase, N * D * (I8PV ? 1 : 2), (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
     auto issue = [&](int st) { issue_at(st, st % RING); };
@@ -651,8 +681,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int d = 32 * m + col;
         return *reinterpret_cast<const v8h*>(L + KBYTES + par * 64 * D + d * 64 + 16 * swz_pos<64>(d, 2 * ks + half));
     };
+    auto vop8_at = [&](int slot, int par, int m) {  // FL_I8PV: the i8 V^T operand of d-block m (all 32 keys)
+        const int8_t* L = lds[slot];
+        const int d = 32 * m + col;
+        return *reinterpret_cast<const v4i*>(L + KBYTES + par * 32 * D + d * 32 + 16 * swz_pos<32>(d, half));
+    };
     auto kop_of = [&](int t, int ks) { return kop_at((t >> 1) % RING, t & 1, ks); };
     auto vop_of = [&](int t, int m, int ks) { return vop_at((t >> 1) % RING, t & 1, m, ks); };
+    auto vop8_of = [&](int t, int m) { return vop8_at((t >> 1) % RING, t & 1, m); };
 
     v16i magic_blk;
 #pragma unroll
@@ -665,7 +701,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // follow chunk c, in kOps order.  Every chained pair (same accumulator) is split by VALU.
     constexpr int MB = D / 32;  // 32-wide d-blocks of O^T (PV accumulators)
     constexpr int KS = D / 32;  // 32-deep k-steps of the i8 Q@K^T
-    constexpr int NOPS = 2 * MB + KS;
+    constexpr int NOPS = (I8PV ? 1 : 2) * MB + KS;
     constexpr int kSlot64[6] = {1, 1, 1, 1, 1, 1};
     constexpr int kOps64[6] = {0, 2, 1, 1000, 3, 1001};  // PV00 PV10 PV01 QK0 PV11 QK1
     constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
@@ -674,10 +710,24 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // d = 128: A PV00 PV10 | B PV20 QK0 | C PV30 PV01 | D QK1 PV11 | E PV21 QK2 | F PV31 QK3 -- every
     // chained pair (PV(m,0) -> PV(m,1), QK(k) -> QK(k+1)) is separated by a VALU chunk and another MFMA
     constexpr int kOps128[12] = {0, 2, 4, 1000, 6, 1, 1001, 3, 5, 1002, 7, 1003};
-    auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
-    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]); };
+    // FL_I8PV: one i8 P@V MFMA per d-block (op 2m), the Q@K^T chain split by VALU chunks as above
+    constexpr int kSlot64i[6] = {1, 1, 0, 1, 0, 1};
+    constexpr int kOps64i[4] = {0, 2, 1000, 1001};  // PV0 PV1 QK0 QK1
+    constexpr int kSlot32i[6] = {1, 0, 0, 1, 0, 0};
+    constexpr int kOps32i[2] = {0, 1000};  // PV0 QK0
+    constexpr int kSlot128i[6] = {2, 1, 2, 1, 1, 1};
+    constexpr int kOps128i[8] = {0, 2, 1000, 4, 1001, 6, 1002, 1003};  // A PV0 PV1 | B QK0 | C PV2 QK1 | D PV3 | E QK2 | F QK3
+    auto slot_n = [&](int c) {
+        if constexpr (I8PV) return D == 32 ? kSlot32i[c] : (D == 64 ? kSlot64i[c] : kSlot128i[c]);
+        else return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]);
+    };
+    auto op_at = [&](int i) {
+        if constexpr (I8PV) return D == 32 ? kOps32i[i] : (D == 64 ? kOps64i[i] : kOps128i[i]);
+        else return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]);
+    };
     static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
-    static_assert(NOPS == (D == 32 ? 3 : (D == 64 ? 6 : 12)), "MFMA schedule table");
+    static_assert(NOPS == (I8PV ? (D == 32 ? 2 : (D == 64 ? 4 : 8)) : (D == 32 ? 3 : (D == 64 ? 6 : 12))),
+                  "MFMA schedule table");
 
     v16f o[MB];                  // O^T, d-block m (anchored)
 #pragma unroll
@@ -690,6 +740,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
     };
     v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
+    v4i pc8, pp8;                // FL_I8PV: the P^T operand as bytes (all 32 keys) of tiles t and t-1
     float scale_prev = 0.0f;
     v16f a[MB];                  // P@V accumulators of the pending tile
     constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
@@ -733,7 +784,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
         h_invp = __builtin_amdgcn_rcpf(sp);
         h_invp *= h_f;
-        h_sp = sp * 16777216.0f;
+        h_sp = I8PV ? sp : sp * 16777216.0f;  // FL_I8PV: P@V is the integer T itself
     };
 
     issue(0);
@@ -757,6 +808,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
         const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
         auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
+        auto vop8 = [&](int m) { return vop8_at(slot_p, par_p, m); };            // tile t-1 (FL_I8PV)
         auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
         const int dma_st = (t >> 1) + PF;
         const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
@@ -773,12 +825,18 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         }
         // operand reads for this iteration's MFMAs (JIT: right before each MFMA instead)
         v8h vv[MB][2];
+        v4i vv8[MB];
         v4i kk[KS];
         if constexpr (has_prev && !JIT) {
+            if constexpr (I8PV) {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
+                for (int m = 0; m < MB; ++m) vv8[m] = vop8(m);
+            } else {
 #pragma unroll
-                for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
+            }
         }
         if constexpr (has_next && !JIT) {
 #pragma unroll
@@ -801,6 +859,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                             if constexpr (PT) {  // P@V straight into O
                                 o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks], o[m], 0,
                                                                               0, 0);
+                            } else if constexpr (I8PV) {  // T + 1.5 * 2^23 in every int32 lane (|T| < 2^22)
+                                a[m] = __builtin_bit_cast(v16f, __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                                    JIT ? vop8(m) : vv8[m], pp8, magic_blk, 0, 0, 0));
                             } else {
                                 a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
                                                                               ks == 0 ? v16f{} : a[m], 0, 0, 0);
@@ -860,12 +921,24 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // and those low 16 bits are exactly the f16 encoding of Pi * 2^-24; one byte permute
         // packs two entries.  P@V then yields T * 2^-24 exactly (T < 2^20); the O scale
         // carries the 2^24 back.
+        if constexpr (I8PV) {  // FL_I8PV: byte e of dword k = Pi of S register 4k + e (the i8 B operand's slot order)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
-            const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
-            pc[r >> 2][2 * (r & 3)] = h2[0];
-            pc[r >> 2][2 * (r & 3) + 1] = h2[1];
+            for (int k4 = 0; k4 < 4; ++k4) {
+                uint32_t tq[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) tq[e] = __float_as_uint(fmaf(p[4 * k4 + e], invp, QMHA_MAGIC_RNE));
+                const uint32_t t01 = __builtin_amdgcn_perm(tq[1], tq[0], 0x0c0c0400u);
+                const uint32_t t23 = __builtin_amdgcn_perm(tq[3], tq[2], 0x0c0c0400u);
+                pc8[k4] = (int)__builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
+                const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
+                pc[r >> 2][2 * (r & 3)] = h2[0];
+                pc[r >> 2][2 * (r & 3) + 1] = h2[1];
+            }
         }
         QMHA_FENCE();
         mfmas(5);
@@ -878,7 +951,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         else
             l_run = fmaf(rs, e * h_f, l_run);
         m_run = m_new;
-        const float scale_t = PT ? 0.0f : sp * svb[t] * e;  // sp carries 2^24: P entries are Pi * 2^-24
+        // sp carries 2^24 (P entries are Pi * 2^-24) except under FL_I8PV (P@V is T itself): the same products,
+        // scaled by 2^24 exactly, so both forms fold the same rounded values
+        const float scale_t = PT ? 0.0f : sp * svb[t] * e;
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor)); PT: O already
         // holds tile t-1's P@V, and takes this tile's alpha before tile t's P@V lands next iteration
         if constexpr (PT) {
@@ -889,13 +964,24 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         } else if constexpr (has_prev) {
 #pragma unroll
             for (int m = 0; m < MB; ++m)
+                if constexpr (I8PV) {  // o += T * s with T = A - 1.5 * 2^23 (exact), packed
 #pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
+                    for (int r = 0; r < 16; r += 2) {
+                        const v2f tt = v2f{a[m][r], a[m][r + 1]} - v2f{QMHA_MAGIC_RNE, QMHA_MAGIC_RNE};
+                        const v2f u = __builtin_elementwise_fma(tt, v2f{scale_prev, scale_prev}, v2f{o[m][r], o[m][r + 1]});
+                        o[m][r] = u[0];
+                        o[m][r + 1] = u[1];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
+                }
         }
         QMHA_FENCE();
         // rotate the pipeline
         pp[0] = pc[0];
         pp[1] = pc[1];
+        if constexpr (I8PV) pp8 = pc8;
         scale_prev = scale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
@@ -1119,6 +1205,13 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
                 for (int m = 0; m < MB; ++m)
                     o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
+        } else if constexpr (I8PV) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                const v16i ai = __builtin_amdgcn_mfma_i32_32x32x32_i8(vop8_of(t, m), pp8, magic_blk, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[m][r] += (__int_as_float(ai[r]) - QMHA_MAGIC_RNE) * scale_prev;
+            }
         } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -1284,7 +1377,8 @@ static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, 
     if (slots <= 0 || nqb > R) {  // occupancy unknown, or a head longer than a round of an XCD: the split's
                                   // producers would run after their consumers (tests/test_fused_schedule.py);
                                   // the two launches instead
-        hipError_t e = launch_quant_int8(Qf, Kf, Vf, w, w.Vh, 1, B, N, H, D, d_model, stream, /*first_tensor=*/1);
+        hipError_t e = launch_quant_int8(Qf, Kf, Vf, w, w.Vh, (FL & FL_I8PV) ? 0 : 1, B, N, H, D, d_model, stream,
+                                         /*first_tensor=*/1);
         return e != hipSuccess ? e : fa_int8_pipe_launch<D, WAVES, FL>(w, Qf, O, B, N, H, d_model, stream);
     }
     const int nflags = B * H * G;
@@ -1345,15 +1439,29 @@ constexpr int kD64Flags = FL_MAGIC | FL_KFOLD, kD32Flags = FL_MAGIC | FL_KFOLD;
 #define QMHA_INT8_W64 4  // waves per workgroup of the per-block d = 64 kernel (A/B builds: -DQMHA_INT8_W64=12)
 #endif
 constexpr int kD128Flags = FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2, kPtD32Extra = FL_LB4;
+// the per-block pipelined kernels' P@V on the i8 matrix core (FL_I8PV; A/B builds: -DQMHA_INT8_I8PV=0|1)
+#ifndef QMHA_INT8_I8PV
+#define QMHA_INT8_I8PV 0
+#endif
+// (d = 32 / 64; the d = 128 schedule, operands read at their MFMA under a 2-wave budget, spills with it)
+template <int D>
+constexpr int kPbExtra = (QMHA_INT8_I8PV && (D == 32 || D == 64)) ? FL_I8PV : 0;
+// V layout the per-block pre-pass writes for this call: 0 = int8 in the i8 V^T operand order (the pipelined
+// kernels under FL_I8PV), 1 = f16 integers (the f16 P@V form, and the one-tile kernel: N = 32, other d)
+int int8_v_mode(int D, int N) {
+    const bool i8pv = D == 32 ? kPbExtra<32> != 0 : (D == 64 ? kPbExtra<64> != 0 : false);
+    return (i8pv && N / QMHA_GROUP >= 2) ? 0 : 1;
+}
 template <int D>
 constexpr int kAnyFlags = FL_MAGIC | (D > 128 ? FL_LB1 : FL_LB2);
 
 template <int D, int XFL = 0>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream, QkDump dbg = QkDump{}) {
-    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    else if constexpr (D == 64) return fa_int8_pipe_launch<D, QMHA_INT8_W64, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | kPbExtra<32> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 64)
+        return fa_int8_pipe_launch<D, QMHA_INT8_W64, kD64Flags | kPbExtra<64> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | kPbExtra<128> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
@@ -1373,9 +1481,9 @@ hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const f
                                 int N, int H, int D, int d_model, hipStream_t stream) {
     if (!int8_fused_on(D, N) || !w.kv_ready) return hipErrorInvalidValue;
     switch (D) {
-        case 32: return fa_int8_fused_launch<32, 4, kD32Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 64: return fa_int8_fused_launch<64, 4, kD64Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 128: return fa_int8_fused_launch<128, 4, kD128Flags>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        case 32: return fa_int8_fused_launch<32, 4, kD32Flags | kPbExtra<32>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_fused_launch<64, 4, kD64Flags | kPbExtra<64>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
+        case 128: return fa_int8_fused_launch<128, 4, kD128Flags | kPbExtra<128>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -28,6 +28,7 @@ struct Int8Workspace {
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
 int int8_scale_stride(int N);  // scales per head in the int8 workspace (N/32 rounded up to 32)
+int int8_v_mode(int D, int N);  // the per-block pre-pass's V layout for this call (launch_quant_int8 v_mode)
 // The fused per-block call (FL_FUSED): K / V quantised by the main kernel's own workgroups, one
 // launch plus a flag-zeroing one.  int8_fused_on: whether run() takes it (d = 32 / 64 / 128, N >= 64,
 // switched on); set_int8_fused: 0 off (pre-pass + main, the default), 1 on, 2 on with the test rule that
