@@ -498,50 +498,50 @@ __device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g
             vt8_group_store<D, false>(T, vx, 1.0f / sv, lane, vd8);
     } else {
 #pragma unroll
-    for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
-        vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
-    auto v_exact = [&]() {
-        float va = 0.0f;
+        for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
+            vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
+        auto v_exact = [&]() {
+            float va = 0.0f;
 #pragma unroll
-        for (int i = 0; i < NV; ++i)
+            for (int i = 0; i < NV; ++i)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                vx[i][c] = nan_to_zero(vx[i][c]);
-                va = fmaxf(va, fabsf(vx[i][c]));
-            }
-        sv = qmha_scale_from_absmax(wave_max64(va));
-        const float iv = 1.0f / sv;
-        vt_tile_write<D>(T, lane, [&](int a, int c) {
-            v4h h;
+                for (int c = 0; c < 4; ++c) {
+                    vx[i][c] = nan_to_zero(vx[i][c]);
+                    va = fmaxf(va, fabsf(vx[i][c]));
+                }
+            sv = qmha_scale_from_absmax(wave_max64(va));
+            const float iv = 1.0f / sv;
+            vt_tile_write<D>(T, lane, [&](int a, int c) {
+                v4h h;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) h[e] = (_Float16)qmha_quant_i8(vx[4 * a + e][c], iv);
-            return h;
-        });
-    };
-    if (allow_fast) {
-        float va = 0.0f;
+                for (int e = 0; e < 4; ++e) h[e] = (_Float16)qmha_quant_i8(vx[4 * a + e][c], iv);
+                return h;
+            });
+        };
+        if (allow_fast) {
+            float va = 0.0f;
 #pragma unroll
-        for (int i = 0; i < NV; ++i)
-            va = fmaxf(fmaxf(va, fmaxf(fabsf(vx[i][0]), fabsf(vx[i][1]))), fmaxf(fabsf(vx[i][2]), fabsf(vx[i][3])));
-        sv = qmha_scale_from_absmax(wave_max64(va));
-        const float iv = 1.0f / sv;
-        uint32_t hi = 0;
-        vt_tile_write<D>(T, lane, [&](int a, int c) {  // rows 4a .. 4a + 3 of this lane's NV, column c
-            const v2f u01 = q2(vx[4 * a][c], vx[4 * a + 1][c], iv, hi);
-            const v2f u23 = q2(vx[4 * a + 2][c], vx[4 * a + 3][c], iv, hi);
-            const v2f y01 = u01 - v2f{Mv, Mv}, y23 = u23 - v2f{Mv, Mv};  // exact integers
-            const v2h h01 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y01[0], y01[1]));
-            const v2h h23 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y23[0], y23[1]));
-            return v4h{h01[0], h01[1], h23[0], h23[1]};
-        });
-        if (__builtin_amdgcn_ballot_w64(hi > kHi)) v_exact();
-    } else {
-        v_exact();
-    }
-    if (coh)
-        vt_tile_store<D, true>(T, lane, vd);
-    else
-        vt_tile_store<D, false>(T, lane, vd);
+            for (int i = 0; i < NV; ++i)
+                va = fmaxf(fmaxf(va, fmaxf(fabsf(vx[i][0]), fabsf(vx[i][1]))), fmaxf(fabsf(vx[i][2]), fabsf(vx[i][3])));
+            sv = qmha_scale_from_absmax(wave_max64(va));
+            const float iv = 1.0f / sv;
+            uint32_t hi = 0;
+            vt_tile_write<D>(T, lane, [&](int a, int c) {  // rows 4a .. 4a + 3 of this lane's NV, column c
+                const v2f u01 = q2(vx[4 * a][c], vx[4 * a + 1][c], iv, hi);
+                const v2f u23 = q2(vx[4 * a + 2][c], vx[4 * a + 3][c], iv, hi);
+                const v2f y01 = u01 - v2f{Mv, Mv}, y23 = u23 - v2f{Mv, Mv};  // exact integers
+                const v2h h01 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y01[0], y01[1]));
+                const v2h h23 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y23[0], y23[1]));
+                return v4h{h01[0], h01[1], h23[0], h23[1]};
+            });
+            if (__builtin_amdgcn_ballot_w64(hi > kHi)) v_exact();
+        } else {
+            v_exact();
+        }
+        if (coh)
+            vt_tile_store<D, true>(T, lane, vd);
+        else
+            vt_tile_store<D, false>(T, lane, vd);
     }
     store_scales(sk, sv);
     if (coh)
