@@ -145,15 +145,18 @@ def test_int8_default_call_is_fused_and_equals_two_launch(dev):
     assert not torch.equal(ref0, ref1)
 
 
-@pytest.mark.parametrize("B,N,H,d", [(2, 1024, 8, 64), (1, 512, 4, 32), (2, 512, 2, 128)])
-def test_int8_fused_nan_inf_groups_bit_identical(dev, B, N, H, d):
+@pytest.mark.parametrize("variant,B,N,H,d", [("fa_tc_int8_b", 2, 1024, 8, 64), ("fa_tc_int8_b", 1, 512, 4, 32),
+                                             ("fa_tc_int8_b", 2, 512, 2, 128), ("fa_tc_v1a", 2, 1024, 8, 64)])
+def test_fused_nan_inf_groups_bit_identical(dev, variant, B, N, H, d):
     """The fused producer's fast quantiser detects a NaN or an infinity in a K / V group from its magic-biased
     results and redoes that group exactly (NaN -> 0, an infinity makes the group scale inf and every value 0,
     as the reference's fp32_to_int8sram).  Groups with NaN / +-inf in K and V, one group all-NaN: the fused call
-    equals the two-launch call bit for bit, on a poisoned caller workspace."""
+    equals the two-launch call bit for bit, on a poisoned caller workspace.  The fp16 form converts NaN / inf
+    as the pre-pass does (RNE), so its NaNs propagate identically."""
     from quantizedmha_amd import _lib
     lib = _lib.load()
-    vid = _lib.variant_id("fa_tc_int8_b")
+    vid = _lib.variant_id(variant)
+    set_fused = lib.qmha_debug_set_int8_fused if variant == "fa_tc_int8_b" else lib.qmha_debug_set_f16_fused
     dm = H * d
     stream = torch.cuda.current_stream(dev).cuda_stream
     g = torch.Generator(device=dev).manual_seed(5)
@@ -171,14 +174,14 @@ def test_int8_fused_nan_inf_groups_bit_identical(dev, B, N, H, d):
 
     def call(fused):
         O = torch.empty_like(Q)
-        prev = lib.qmha_debug_set_int8_fused(fused)
+        prev = set_fused(fused)
         try:
             ws.random_(0, 256)
             _lib.check(lib.qmha_solve_ws(Q.data_ptr(), K.data_ptr(), V.data_ptr(), O.data_ptr(), B, N, dm, H, vid,
                                          ws.data_ptr(), ws.numel(), stream))
             torch.cuda.synchronize()
         finally:
-            lib.qmha_debug_set_int8_fused(prev)
+            set_fused(prev)
         return O
 
     ref, out = call(0), call(1)
