@@ -412,12 +412,21 @@ static hipError_t fa_f16_fused_launch(const F16Workspace& w, const float* Qf, co
     const int G = N / QMHA_GROUP;
     const int nqb = (G + WAVES - 1) / WAVES;
     const long long nwg = (long long)B * H * nqb;
-    int occ = 0, cus = 0, dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qmha_fa_f16_v2_kernel<D, WAVES, SG, FLF>, WAVES * 64, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        occ = 0;
-    const int R = occ * cus / 8;
+    // resident workgroups per XCD (HIP's occupancy answer x CUs / 8), cached per device; 0 if unknown
+    static std::atomic<int> r_of[64];
+    int dev = 0, R = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        R = r_of[dev].load(std::memory_order_relaxed);
+        if (R <= 0) {
+            int occ = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qmha_fa_f16_v2_kernel<D, WAVES, SG, FLF>, WAVES * 64, 0) ==
+                    hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ > 0 && cus > 0) {
+                R = occ * cus / 8;
+                r_of[dev].store(R, std::memory_order_relaxed);
+            }
+        }
+    }
     if (R <= 0 || nqb > R || nwg > INT32_MAX) {  // occupancy unknown or a head longer than a round: two launches
         hipError_t e = launch_convert_f16(Qf, Kf, Vf, w, B, N, H, D, d_model, stream);
         return e != hipSuccess ? e : fa_f16_v2_launch<D, WAVES, SG, FL>(w, Qf, O, B, N, H, d_model, stream);
