@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Extended parity sweep on the GPU (evidence beyond the pytest suite, not part of it): random shapes
+(B 1..6, N = 32 * (1..96), H 1..8, d in {32, 64, 128}, N(0, 0.5^2) or U[0, 1) inputs) through every
+fused-attention variant against the oracle, at the suite's criteria (tests/test_gpu_parity.py
+assert_parity); for fa_tc_int8_b and fa_tc_v1a also the one-launch opt-ins, which must equal the default
+call bit for bit.  Test infrastructure: the oracle is the checker.
+    python tools/r05/sweep.py [--n 200] [--seed 5]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import oracle as oracle_mod  # noqa: E402
+from quantizedmha_amd import _lib, torch_ext  # noqa: E402
+from tests.test_gpu_parity import INT8_TOL_TIGHT, INT8_FLIP_FRAC, INT8_FLIP_FRAC_PT, TOL_ORACLE, int8_tol  # noqa: E402
+
+VARIANTS = ("fa_tc_int8_b", "fa_tc_int8_pt", "fa_tc_v1a", "fa")
+
+
+def check(variant, out, ref, N):
+    err = np.abs(out.astype(np.float64) - ref.astype(np.float64))
+    if not np.isfinite(out).all():
+        return False, float("inf"), 1.0
+    tol = int8_tol(N) if variant in ("fa_tc_int8_b", "fa_tc_int8_pt") else TOL_ORACLE[variant]
+    frac = float((err > INT8_TOL_TIGHT).mean())
+    ok = err.max() <= tol
+    if variant == "fa_tc_int8_b":
+        ok = ok and frac <= INT8_FLIP_FRAC
+    if variant == "fa_tc_int8_pt":
+        ok = ok and frac <= INT8_FLIP_FRAC_PT
+    return ok, float(err.max()), frac
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=5)
+    a = ap.parse_args()
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(a.seed)
+    fails, worst = 0, {v: 0.0 for v in VARIANTS}
+    t0 = time.time()
+    for i in range(a.n):
+        while True:
+            d = int(rng.choice([32, 64, 128]))
+            G, H, B = int(rng.integers(1, 97)), int(rng.integers(1, 9)), int(rng.integers(1, 7))
+            if B * H * (32 * G) ** 2 * d <= 1.5e9:
+                break
+        N, dm = 32 * G, H * d
+        shape = (B, N, dm) if B > 1 else (N, dm)
+        if i % 2:
+            Q, K, V = [(rng.standard_normal(shape) * 0.5).astype(np.float32) for _ in range(3)]
+        else:
+            Q, K, V = [rng.random(shape, dtype=np.float32) for _ in range(3)]
+        t = [torch.from_numpy(x).to(dev) for x in (Q, K, V)]
+        line = [f"{i:3d} B{B} N{N} H{H} d{d} {'N' if i % 2 else 'U'}:"]
+        for v in VARIANTS:
+            ref = oracle_mod.ORACLE_BY_VARIANT[v](Q, K, V, dm, H, nthreads=16)
+            out = torch_ext.flash_solve(t[0], t[1], t[2], dm, H, kernel=v)
+            torch.cuda.synchronize()
+            ok, e, frac = check(v, out.cpu().numpy(), ref, N)
+            worst[v] = max(worst[v], e)
+            fused = ""
+            if v in ("fa_tc_int8_b", "fa_tc_v1a"):
+                setf = lib.qmha_debug_set_int8_fused if v == "fa_tc_int8_b" else lib.qmha_debug_set_f16_fused
+                prev = setf(1)
+                try:
+                    out_f = torch_ext.flash_solve(t[0], t[1], t[2], dm, H, kernel=v)
+                    torch.cuda.synchronize()
+                finally:
+                    setf(prev)
+                same = torch.equal(out_f, out)
+                ok = ok and same
+                fused = " fused=" + ("same" if same else "DIFF")
+            fails += not ok
+            line.append(f"{v} {e:.2e}/{frac:.1e}{fused}{'' if ok else ' FAIL'}")
+        print(" ".join(line), flush=True)
+    print(f"{a.n} shapes, {fails} failures, {time.time() - t0:.0f} s; worst max|gpu - oracle|: " +
+          ", ".join(f"{v} {e:.2e}" for v, e in worst.items()), flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()
