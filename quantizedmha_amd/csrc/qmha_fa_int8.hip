@@ -40,6 +40,10 @@
 #include <atomic>
 #include <type_traits>
 
+#ifndef QMHA_FOLD_PK
+#define QMHA_FOLD_PK 0  // A/B builds: -DQMHA_FOLD_PK=1, the per-block O fold as packed fp32 fmas
+#endif
+
 namespace qmha {
 
 // log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
@@ -973,8 +977,18 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                         o[m][r + 1] = u[1];
                     }
                 } else {
+#if QMHA_FOLD_PK  // A/B: the fold as packed fp32 fmas (16 v_pk_fma instead of 32 v_fmac per d-block)
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {
+                        const v2f u = __builtin_elementwise_fma(v2f{a[m][r], a[m][r + 1]}, v2f{scale_prev, scale_prev},
+                                                                v2f{o[m][r], o[m][r + 1]});
+                        o[m][r] = u[0];
+                        o[m][r + 1] = u[1];
+                    }
+#else
 #pragma unroll
                     for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
+#endif
                 }
         }
         QMHA_FENCE();
