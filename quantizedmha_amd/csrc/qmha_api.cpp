@@ -5,6 +5,8 @@
 // heads in one grid, and errors are reported instead of ignored.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -34,6 +36,46 @@ int hip_fail(hipError_t e, const char* what) {
         hipError_t _e = (expr);                  \
         if (_e != hipSuccess) return hip_fail(_e, what); \
     } while (0)
+
+// Blocking wait for the null stream's work so far (solve()'s semantics, reference launchers.h:64): a
+// stream-ordered write of a per-thread sequence number into pinned host memory (hipStreamWriteValue32:
+// performed after all earlier commands of the stream have completed), spun on by this thread, with a
+// hipStreamQuery every few thousand spins so that a failed stream ends the wait.  hipStreamSynchronize
+// when the write is unavailable.  The pinned word is per host thread (concurrent callers) and never
+// freed (it may outlive the HIP runtime at exit).
+struct HostFlag {
+    uint32_t* p = nullptr;
+    uint32_t seq = 0;
+    bool usable = true;
+};
+thread_local HostFlag t_flag;
+
+hipError_t wait_null_stream() {
+    if (t_flag.usable && !t_flag.p) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess || !p) {
+            t_flag.usable = false;
+        } else {
+            t_flag.p = static_cast<uint32_t*>(p);
+            __atomic_store_n(t_flag.p, 0u, __ATOMIC_RELEASE);
+        }
+    }
+    if (t_flag.usable) {
+        const uint32_t v = ++t_flag.seq;
+        if (hipStreamWriteValue32(nullptr, t_flag.p, v, 0) == hipSuccess) {
+            for (unsigned i = 1;; ++i) {
+                if (__atomic_load_n(t_flag.p, __ATOMIC_ACQUIRE) == v) return hipSuccess;
+                if ((i & 4095u) == 0) {
+                    const hipError_t q = hipStreamQuery(nullptr);
+                    if (q != hipErrorNotReady) return q == hipSuccess ? hipStreamSynchronize(nullptr) : q;
+                }
+                _mm_pause();
+            }
+        }
+        t_flag.usable = false;
+    }
+    return hipStreamSynchronize(nullptr);
+}
 
 int check_shape(const void* Q, const void* K, const void* V, const void* O, int B, int N, int d_model, int h,
                 int variant, int* D_out) {
@@ -380,12 +422,14 @@ size_t qmha_workspace_size(int B, int N, int d_model, int h, int variant) {
 
 int qmha_solve_variant(const float* Q, const float* K, const float* V, float* O, int N, int d_model, int h,
                        int variant) {
-    // blocking like the reference (launchers.h:64); r04 A/B: polling hipStreamQuery on the null stream
-    // (2.01 ms per 16 calls at C4) or on a library-owned stream (2.06 ms) instead of this
-    // hipStreamSynchronize (1.94 ms) was slower (profiles/r04/ab_sync/summary.txt)
+    // blocking like the reference (launchers.h:64).  r04 A/B: polling hipStreamQuery on the null stream
+    // (2.01 ms per 16 calls at C4) or on a library-owned stream (2.06 ms) was slower than
+    // hipStreamSynchronize (1.94 ms, profiles/r04/ab_sync/summary.txt); r05: a stream-ordered host-flag
+    // write spun on (wait_null_stream) against hipStreamSynchronize, same box: 1.868 vs 1.883 ms per 16 C4
+    // calls, fp16 1.897 vs 1.919 ms (profiles/r05/ab_solve_sync/)
     int st = qmha_solve_ex(Q, K, V, O, 1, N, d_model, h, variant, nullptr);
     if (st != QMHA_OK) return st;
-    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    QMHA_HIP_TRY(wait_null_stream(), "solve: waiting for the null stream");
     return QMHA_OK;
 }
 
