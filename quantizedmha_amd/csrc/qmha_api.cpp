@@ -53,7 +53,7 @@ thread_local HostFlag t_flag;
 hipError_t wait_null_stream() {
     if (t_flag.usable && !t_flag.p) {
         void* p = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess || !p) {
+        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !p) {
             t_flag.usable = false;
         } else {
             t_flag.p = static_cast<uint32_t*>(p);
