@@ -589,7 +589,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     constexpr bool PT = FL & FL_PT;
     constexpr bool FUSED = FL & FL_FUSED;
     static_assert(!(FUSED && (PT || DUMP)), "FL_FUSED: the per-block production kernel only");
-    static_assert(!(I8PV && PT), "FL_I8PV: the per-block contract (the per-tensor P@V accumulates across tiles)");
+    // PT + FL_I8PV (A/B builds, -DQMHA_INT8_PT_I8PV=1): the per-tensor P@V on the i8 matrix core into an int32
+    // window that is folded into O when a row's running max moves (iter_pt)
+    constexpr bool PT8 = PT && I8PV;
+    static_assert(!PT8 || D == 32 || D == 64, "FL_PT | FL_I8PV: d = 32 / 64");
     if constexpr (FUSED) {
         // the K / V groups (qmha_fused.hpp); each wave's LDS transpose tile sits in the ring, which is not
         // in use before the first DMA below (fused_produce_and_wait ends with a workgroup barrier)
@@ -1007,6 +1010,39 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
     // P@V of t-2 has), so no MFMA result is waited on.
     float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
+    // PT8: P@V of the tiles since the last fold accumulates exactly in the int32 window w8 (every tile of a
+    // window quantised against the same running max m_w).  When some row's max moves, the window is folded
+    // into O in anchor units, o += W * 2^(m_w - anchor) (one conversion and one fma per element, no O
+    // rescale: the anchored O of the per-block kernel), and restarted.  |W| < 2^31 for up to 4160 tiles
+    // of 32 keys (32 * 127 * 127 each): int8_pt_v8 limits N to 131072.
+    v16i w8[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) w8[m] = v16i{};
+    float m_w = 0.0f, f_w = 1.0f;
+    auto fold8 = [&]() {
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[m][r] = fmaf((float)w8[m][r], f_w, o[m][r]);
+            // restart the window: 8 64-bit moves per d-block (the compiler's zeroing is 16 32-bit ones)
+            v2i z[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("v_mov_b64 %0, 0" : "=v"(z[i]));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                w8[m][2 * i] = z[i][0];
+                w8[m][2 * i + 1] = z[i][1];
+            }
+        }
+        m_w = m_run;
+        if (__builtin_amdgcn_ballot_w64(m_w - anchor > 48.0f)) {  // keep 2^(m - anchor) <= 2^48 (rare)
+            const float g = __builtin_amdgcn_exp2f(anchor - m_w);
+#pragma unroll
+            for (int m = 0; m < MB; ++m) o[m] *= g;
+            anchor = m_w;
+        }
+        f_w = __builtin_amdgcn_exp2f(m_w - anchor);
+    };
     auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
         constexpr int ph = decltype(PH)::value;
@@ -1029,14 +1065,20 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         v8h vv[MB][2];
+        v4i vv8[MB];
         v4i kk[KS];
-        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs
+        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs (PT8: the k-step-0 P@V slots, one i8 MFMA per d-block)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int op = pt_slot_op(D, s, j);
                 if (op >= 0 && op < 8) {
-                    if constexpr (has_prev)
-                        if ((op >> 1) < MB) vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
+                    if constexpr (has_prev) {
+                        if constexpr (PT8) {
+                            if ((op & 1) == 0 && (op >> 1) < MB) vv8[(op >> 1) % MB] = vop8_at(slot_p, par_p, op >> 1);
+                        } else if ((op >> 1) < MB) {
+                            vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
+                        }
+                    }
                 } else if (op >= 8) {
                     if constexpr (has_next)
                         if (op - 8 < KS) kk[(op - 8) % KS] = kop_at(slot_nx, par_n, op - 8);
@@ -1048,11 +1090,15 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             for (int j = 0; j < 2; ++j) {
                 const int op = pt_slot_op(D, s, j);
                 if (op >= 0 && op < 8) {
-                    if constexpr (has_prev)
-                        if ((op >> 1) < MB) {
-                            const int m = (op >> 1) % MB;
+                    if constexpr (has_prev) {
+                        const int m = (op >> 1) % MB;
+                        if constexpr (PT8) {
+                            if ((op & 1) == 0 && (op >> 1) < MB)
+                                w8[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vv8[m], pp8, w8[m], 0, 0, 0);
+                        } else if ((op >> 1) < MB) {
                             o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][op & 1], pp[op & 1], o[m], 0, 0, 0);
                         }
+                    }
                 } else if (op >= 8) {
                     if constexpr (has_next)
                         if (op - 8 < KS) qk(kk[(op - 8) % KS], op - 8);
@@ -1071,6 +1117,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
         };
         auto perms = [&](int j0, int j1) {
+            if constexpr (PT8) {  // bytes: byte e of dword k = Pi of S register 4k + e (the i8 B operand's slot order)
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4)
+                    if (2 * k4 >= j0 && 2 * k4 < j1) {
+                        const uint32_t t01 = __builtin_amdgcn_perm(__float_as_uint(q[4 * k4 + 1]), __float_as_uint(q[4 * k4]), 0x0c0c0400u);
+                        const uint32_t t23 = __builtin_amdgcn_perm(__float_as_uint(q[4 * k4 + 3]), __float_as_uint(q[4 * k4 + 2]), 0x0c0c0400u);
+                        pc8[k4] = (int)__builtin_amdgcn_perm(t23, t01, 0x05040100u);
+                    }
+                asm volatile("" : "+v"(pc8));
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (j >= j0 && j < j1) {
@@ -1089,7 +1146,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float c = h_c, kn = h_k;
         QMHA_FENCE();
         if constexpr (has_prev) {
-            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+            if constexpr (PT8) {  // the window's tiles (<= t-2) and tile t-1 were quantised against different maxima
+                if (__builtin_amdgcn_ballot_w64(m_run != m_w)) fold8();
+            } else if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
             }
@@ -1154,8 +1213,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         QMHA_FENCE();
         mf_slot(5);
         QMHA_FENCE();
-        pp[0] = pc[0];
-        pp[1] = pc[1];
+        if constexpr (PT8) {
+            pp8 = pc8;
+        } else {
+            pp[0] = pc[0];
+            pp[1] = pc[1];
+        }
         alpha_prev = h_alpha;
         if constexpr (has_next) s_cur = s_nxt;
     };
@@ -1209,7 +1272,15 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // drain: P@V of the last tile
     {
         const int t = G - 1;
-        if constexpr (PT) {
+        if constexpr (PT8) {
+            if (__builtin_amdgcn_ballot_w64(m_run != m_w)) fold8();
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                w8[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vop8_of(t, m), pp8, w8[m], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf((float)w8[m][r], f_w, o[m][r]);
+            }
+        } else if constexpr (PT) {
             if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {  // O still owes the last tile's alpha
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
@@ -1241,7 +1312,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     if (active) {
         // PT: O is in units of 2^-24 (the f16-subnormal P entries) times sV / 127: 2^24 * sV / 127
         // rescales it exactly to the oracle's O * (sV / 127)
-        const float unanchor = PT ? 16777216.0f * (svb[0] / 127.0f) : __builtin_amdgcn_exp2f(anchor - m_run);
+        // PT8: O is in units of sV / 127 times 2^(m - anchor)
+        const float unanchor = PT8  ? __builtin_amdgcn_exp2f(anchor - m_run) * (svb[0] / 127.0f)
+                               : PT ? 16777216.0f * (svb[0] / 127.0f)
+                                    : __builtin_amdgcn_exp2f(anchor - m_run);
         const float l = PT ? half_swap_add(l_run) : half_swap_add(l_run) * unanchor;
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
@@ -1479,8 +1553,19 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
+// the per-tensor kernels' P@V on the i8 matrix core into an int32 window (PT + FL_I8PV; A/B builds:
+// -DQMHA_INT8_PT_I8PV=0|1, qmha_kernels.hpp; d = 32 / 64, at least two tiles, N <= 131072 for the window's int32 range)
+bool int8_pt_v8(int D, int N) {
+    return QMHA_INT8_PT_I8PV && (D == 32 || D == 64) && N / QMHA_GROUP >= 2 && N <= 131072;
+}
+
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, hipStream_t stream) {
+#if QMHA_INT8_PT_I8PV
+    if (int8_pt_v8(D, N))
+        return D == 32 ? fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_I8PV>(w, Qf, O, B, N, H, d_model, stream)
+                       : fa_int8_pt_launch<64, kD64Flags | FL_I8PV>(w, Qf, O, B, N, H, d_model, stream);
+#endif
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra>(w, Qf, O, B, N, H, d_model, stream);
         case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
@@ -1531,6 +1616,11 @@ hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O
 // launch_fa_int8_pt_main, plus the stores)
 hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, QkDump dbg, hipStream_t stream) {
+#if QMHA_INT8_PT_I8PV  // the production instance's twin (the pre-pass wrote V for it)
+    if (int8_pt_v8(D, N))
+        return D == 32 ? fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_I8PV | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg)
+                       : fa_int8_pt_launch<64, kD64Flags | FL_I8PV | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+#endif
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 64: return fa_int8_pt_launch<64, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);

@@ -50,6 +50,12 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
 // layout: Ki, Vh as fa_tc_int8_b, then slice_sync [2][3][B*H] uint32, then sQ, sK, sV [B*H] each
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D);
+// whether this call's per-tensor main kernel runs P@V on the i8 matrix core (FL_I8PV, A/B builds
+// -DQMHA_INT8_PT_I8PV=1; d = 32 / 64): then the pre-pass writes V as int8 in the i8 V^T operand order
+#ifndef QMHA_INT8_PT_I8PV
+#define QMHA_INT8_PT_I8PV 0
+#endif
+bool int8_pt_v8(int D, int N);
 // one pass: K / V quantised with their head-slice scales from registers, sQ (qmha_pt_quant_kernel)
 // the per-tensor pre-pass's bounded wait in 100 MHz ticks (default 200000 = 2 ms; 0 forces the
 // fallback); returns the previous value

@@ -8,7 +8,8 @@ f16 MFMA's 128) -- but only between two changes of a row's running max: when any
 (alpha != 1), the int32 window must be folded into the fp32 O (O = alpha (O + float(acc)), acc = 0).  This
 script measures how often that happens on the bench's inputs and prices both schedules with the measured
 gfx950 issue costs (2.4 cycles per full-rate fp32 op, 4.0 per cvt / perm / mov-class op,
-30-32 per 32x32 MFMA).
+30-32 per 32x32 MFMA).  Built afterwards with a cheaper fold (O kept in anchor units, no rescale) as the A/B
+build QMHA_INT8_PT_I8PV=1 and measured +3 % at C4 (profiles/r05/ab_pt_i8pv/).
 
     python tools/pt_int8pv_model.py
 """
