@@ -4,7 +4,7 @@
 fused-attention variant against the oracle, at the suite's criteria (tests/test_gpu_parity.py
 assert_parity); for fa_tc_int8_b and fa_tc_v1a also the one-launch opt-ins, which must equal the default
 call bit for bit.  Test infrastructure: the oracle is the checker.
-    python tools/r05/sweep.py [--n 200] [--seed 5]"""
+    python tools/r05/sweep.py [--n 200] [--seed 5] [--variants fa_tc_int8_pt]"""
 import argparse
 import os
 import sys
@@ -41,11 +41,14 @@ def main():
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--only", type=int, default=-1, help="run shape i only (the earlier draws are consumed)")
+    ap.add_argument("--variants", default=",".join(VARIANTS), help="comma-separated subset of " + ",".join(VARIANTS))
     a = ap.parse_args()
+    variants = [v for v in a.variants.split(",") if v]
+    assert variants and all(v in VARIANTS for v in variants), variants
     lib = _lib.load()
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(a.seed)
-    fails, worst = 0, {v: 0.0 for v in VARIANTS}
+    fails, worst = 0, {v: 0.0 for v in variants}
     t0 = time.time()
     for i in range(a.n):
         while True:
@@ -63,7 +66,7 @@ def main():
             continue
         t = [torch.from_numpy(x).to(dev) for x in (Q, K, V)]
         line = [f"{i:3d} B{B} N{N} H{H} d{d} {'N' if i % 2 else 'U'}:"]
-        for v in VARIANTS:
+        for v in variants:
             ref = oracle_mod.ORACLE_BY_VARIANT[v](Q, K, V, dm, H, nthreads=16)
             out = torch_ext.flash_solve(t[0], t[1], t[2], dm, H, kernel=v)
             torch.cuda.synchronize()
