@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -255,6 +256,91 @@ def _cpu_model():
     return "unknown"
 
 
+def clock_probe(dev):
+    """The shader clock under an MFMA + VALU mix like the int8 main kernel's (libqmha_probe.so,
+    quantizedmha_amd/csrc/qmha_clock_probe.hip: s_memtime cycles / s_memrealtime ticks, in-kernel), run right
+    after the headline so it sees the same thermal / power state."""
+    import ctypes
+    path = os.path.join(ROOT, "quantizedmha_amd", "lib", "libqmha_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.qmha_clock_probe.restype = ctypes.c_int
+    lib.qmha_clock_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    out = (ctypes.c_double * 4)()
+    st = lib.qmha_clock_probe(5, 20, out)
+    torch.cuda.synchronize(dev)
+    if st != 0:
+        return {"error": f"hip error {st}"}
+    return {"clock_ghz": round(out[0], 4), "ns_per_unit_per_simd": round(out[1], 3),
+            "cycles_per_unit": round(out[2], 2), "timed_ms": round(out[3], 3),
+            "unit": "1 v_mfma_i32_32x32x32_i8 + 3 v_exp_f32 + 21 v_fma_f32, 3 waves/SIMD"}
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def device_state(dev):
+    """This GPU's power cap and power draw from sysfs (hwmon of its PCI function; plain file reads, no
+    rocm-smi), plus the identity torch reports."""
+    import glob
+    p = torch.cuda.get_device_properties(dev)
+    out = {"name": p.name, "arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count}
+    dom, bus, devn = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    hw = []
+    if bus is not None:
+        pci = f"{dom or 0:04x}:{bus:02x}:{devn or 0:02x}.0"
+        out["pci"] = pci
+        hw = glob.glob(f"/sys/bus/pci/devices/{pci}/hwmon/hwmon*")
+    if hw:
+        h = hw[0]
+        for key, fn, scale in (("power_cap_w", "power1_cap", 1e-6), ("power_cap_max_w", "power1_cap_max", 1e-6),
+                               ("power_now_w", "power1_average", 1e-6), ("power_input_w", "power1_input", 1e-6),
+                               ("sclk_mhz", "freq1_input", 1e-6), ("temp_edge_c", "temp1_input", 1e-3),
+                               ("temp_hotspot_c", "temp2_input", 1e-3)):
+            v = _read(os.path.join(h, fn))
+            if v is not None and v.lstrip("-").isdigit():
+                out[key] = round(int(v) * scale, 1)
+        out["hwmon"] = h
+    return out
+
+
+def isa_ids(variant, d):
+    """isa_sha16 of the shipped main kernel and pre-pass of this variant at head size d: the first 16 hex
+    digits of the SHA-256 of their gfx950 instruction bytes in the loaded libqmha.so (quantizedmha_amd/isa_id.py)."""
+    from quantizedmha_amd import isa_id
+    pats = {"fa_tc_int8_b": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_quant_int8_kernelILi{d}ELi1E"),
+            "fa_tc_int8_pt": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_pt_quant_kernelILi{d}E"),
+            "fa_tc_v1a": (f"qmha_fa_f16_v2_kernelILi{d}E", f"qmha_convert_f16_kernelILi{d}E"),
+            "fa": (f"qmha_fa_f32_v3_kernelILi{d}E", None), "fa_mfma": (f"qmha_fa_f32_mfma_kernelILi{d}E", None),
+            "unfused": ("qmha_gemm_f32_mfma_kernel", "qmha_softmax_rows")}.get(variant, (None, None))
+    out = {}
+    for role, pat in zip(("main", "prepass"), pats):
+        if not pat:
+            continue
+        ks = isa_id.kernel_bytes(_lib.LIB_PATH, pat)
+        if variant.startswith("fa_tc_int8"):  # the production instance: FL_DUMP (256) clear, FL_PT (1 << 20) as the variant
+            want_pt = variant == "fa_tc_int8_pt"
+            keep = {}
+            for name, b in ks.items():
+                fl = re.search(r"ILi\d+ELi\d+ELi(\d+)E", name)
+                if role == "main" and fl and (int(fl.group(1)) & 256 or bool(int(fl.group(1)) & (1 << 20)) != want_pt):
+                    continue
+                keep[name] = b
+            ks = keep
+        if ks:
+            name = sorted(ks)[0]
+            import hashlib
+            out[role] = {"isa_sha16": hashlib.sha256(b"".join(ks[k] for k in sorted(ks))).hexdigest()[:16],
+                         "symbols": len(ks), "bytes": sum(len(b) for b in ks.values()), "symbol": name}
+    return out
+
+
 def pmc_traffic(variant, B, H, N, d):
     """HBM bytes per main-kernel launch from the committed rocprofv3 PMC summary
     (profiles/*/pmc_<variant>.json, produced by tools/pmc_summary.py), or None."""
@@ -424,8 +510,6 @@ def main():
         res["dry_run"] = True
     else:
         kname = f"qmha_fa_{'int8' if a.variant == 'fa_tc_int8_b' else a.variant}"
-        if a.variant == "fa_tc_int8_b" and lib_fused_on(d, N):  # one kernel: K/V quantisation + sweep
-            kname = "qmha_fa_int8_pipe_kernel<FL_FUSED> (K/V quantisation inside; + the flag-zeroing launch)"
         res["roofline"] = {"bound": "mfma", "kernel": kname,
                            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -436,6 +520,25 @@ def main():
                            "hbm_algorithmic_bytes_per_call": hbm_alg,
                            "hbm_GBs_per_call": round(hbm_alg / (r["ms_per_step"] * 1e-3) / 1e9, 1),
                            "mfma_busy_pct": busy, "mfma_busy_source": busy_src}
+    if not dry:
+        # reproducibility across boxes (round-5 VERDICT item 2): the clock this box holds under the kernel's
+        # mix, measured right after the headline, its power cap, and the identity of the code that ran
+        probe = clock_probe(dev)
+        dstate = device_state(dev)
+        ids = isa_ids(a.variant, d)
+        res["device"] = dstate
+        res["clock_probe"] = probe
+        res["power_cap_w"] = dstate.get("power_cap_w")
+        res["isa_sha16"] = ids.get("main", {}).get("isa_sha16")
+        res["isa"] = ids
+        ghz = (probe or {}).get("clock_ghz")
+        res["clock_ghz"] = ghz
+        if ghz and r["main_kernel_ms"] > 0:
+            # wave-tiles (32 query rows x 32 keys) per SIMD of one launch
+            tiles = B * H * (N // 32) ** 2 / (dstate["cus"] * 4)
+            res["cycles_per_tile"] = round(r["main_kernel_ms"] * 1e-3 * ghz * 1e9 / tiles, 1)
+            res["roofline"]["cycles_per_tile"] = res["cycles_per_tile"]
+            res["roofline"]["tiles_per_simd"] = tiles
     if dist.is_initialized():
         ag_ms = time_allgather(r["O"], max(3, a.steps // 2), dev, world)
         sg_ms = time_solve_gather(a.variant, r["inputs"], H, d, max(3, a.steps // 2), dev, world,
@@ -485,16 +588,6 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
-
-
-def lib_fused_on(d, N):
-    """Whether the per-block int8 call runs as one fused kernel (qmha_debug_set_int8_fused reads and
-    restores the library's switch).  The fused form is an opt-in (qmha_debug_set_int8_fused(1)); the
-    library's default is the two launches."""
-    lib = _lib.load()
-    mode = lib.qmha_debug_set_int8_fused(1)
-    lib.qmha_debug_set_int8_fused(mode)
-    return mode != 0 and d in (32, 64, 128) and N >= 64
 
 
 def time_quantize_int8(B, H, N, d, dev, steps=20):

@@ -131,23 +131,6 @@ int qmha_debug_fa_int8_pt_dump(const float *Q, const float *K, const float *V, f
  * previous bound. */
 int64_t qmha_debug_set_pt_wait(int64_t ticks);
 
-/* Test hooks of the fused per-block int8 call (fa_tc_int8_b at d = 32 / 64 / 128, N >= 64: the main
- * kernel quantises K / V itself).  mode 0 = two launches (pre-pass, then the main
- * kernel), 1 = fused, 2 = fused with every K / V group produced by a workgroup of another XCD
- * (coherence check); ticks = the bound of a workgroup's wait for its head's groups (100 MHz clock,
- * default 5000; 0 makes every wave produce its share itself).  All give bit-identical output.  Each
- * returns the previous value. */
-int qmha_debug_set_int8_fused(int mode);
-int64_t qmha_debug_set_int8_fused_wait(int64_t ticks);
-/* Measurement hook (results WRONG while nonzero): parts of the fused kernel switched off --
- * bit 0 the wait for the head's groups, bit 1 the agent-coherent stores and their completion wait, bit 2 all
- * production, bit 3 the fast quantiser (the exact path for every group).  Returns the previous bits. */
-int qmha_debug_set_int8_fused_ablate(int bits);
-/* Test hook of the fused fp16 call (fa_tc_v1a at d = 32 / 64 / 128: the main kernel converts K / V itself with
- * the same split and flags).  mode 0 = two launches (the default), 1 = fused, 2 = fused with the
- * cross-XCD test rule.  Bit-identical output.  Returns the previous mode. */
-int qmha_debug_set_f16_fused(int mode);
-
 /* Variant name ("fa", "fa_tc_v1a", "fa_tc_int8_b", "unfused", "fa_mfma", "fa_tc_int8_pt") -> id, or -1. */
 int qmha_variant_from_name(const char *name);
 const char *qmha_variant_name(int variant);

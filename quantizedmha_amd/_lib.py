@@ -36,10 +36,6 @@ SIGNATURES = {
     "qmha_profile_enable": (None, [_i]),
     "qmha_set_overlap_chunks": (_i, [_i]),
     "qmha_debug_set_pt_wait": (ctypes.c_longlong, [ctypes.c_longlong]),
-    "qmha_debug_set_int8_fused": (_i, [_i]),
-    "qmha_debug_set_int8_fused_wait": (ctypes.c_longlong, [ctypes.c_longlong]),
-    "qmha_debug_set_int8_fused_ablate": (_i, [_i]),
-    "qmha_debug_set_f16_fused": (_i, [_i]),
     "qmha_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                   ctypes.POINTER(ctypes.c_double)]),
     "qmha_release_workspaces": (None, []),

@@ -5,15 +5,16 @@
 // heads in one grid, and errors are reported instead of ignored.
 #include <hip/hip_runtime.h>
 
-#include <immintrin.h>
-
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -36,46 +37,6 @@ int hip_fail(hipError_t e, const char* what) {
         hipError_t _e = (expr);                  \
         if (_e != hipSuccess) return hip_fail(_e, what); \
     } while (0)
-
-// Blocking wait for the null stream's work so far (solve()'s semantics, reference launchers.h:64): a
-// stream-ordered write of a per-thread sequence number into pinned host memory (hipStreamWriteValue32:
-// performed after all earlier commands of the stream have completed), spun on by this thread, with a
-// hipStreamQuery every few thousand spins so that a failed stream ends the wait.  hipStreamSynchronize
-// when the write is unavailable.  The pinned word is per host thread (concurrent callers) and never
-// freed (it may outlive the HIP runtime at exit).
-struct HostFlag {
-    uint32_t* p = nullptr;
-    uint32_t seq = 0;
-    bool usable = true;
-};
-thread_local HostFlag t_flag;
-
-hipError_t wait_null_stream() {
-    if (t_flag.usable && !t_flag.p) {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !p) {
-            t_flag.usable = false;
-        } else {
-            t_flag.p = static_cast<uint32_t*>(p);
-            __atomic_store_n(t_flag.p, 0u, __ATOMIC_RELEASE);
-        }
-    }
-    if (t_flag.usable) {
-        const uint32_t v = ++t_flag.seq;
-        if (hipStreamWriteValue32(nullptr, t_flag.p, v, 0) == hipSuccess) {
-            for (unsigned i = 1;; ++i) {
-                if (__atomic_load_n(t_flag.p, __ATOMIC_ACQUIRE) == v) return hipSuccess;
-                if ((i & 4095u) == 0) {
-                    const hipError_t q = hipStreamQuery(nullptr);
-                    if (q != hipErrorNotReady) return q == hipSuccess ? hipStreamSynchronize(nullptr) : q;
-                }
-                _mm_pause();
-            }
-        }
-        t_flag.usable = false;
-    }
-    return hipStreamSynchronize(nullptr);
-}
 
 int check_shape(const void* Q, const void* K, const void* V, const void* O, int B, int N, int d_model, int h,
                 int variant, int* D_out) {
@@ -155,7 +116,7 @@ struct SideStream {
     std::vector<hipEvent_t> ready;
 };
 std::mutex g_side_mu;
-std::map<std::pair<int, void*>, SideStream> g_side;
+std::map<std::tuple<int, void*, std::thread::id>, SideStream> g_side;  // keyed like the workspace slots
 
 std::atomic<int> g_overlap_chunks{-1};  // -1: not yet read from QMHA_OVERLAP_CHUNKS
 
@@ -178,7 +139,7 @@ int get_side(hipStream_t stream, int nchunks, SideStream** out) {
     int dev = 0;
     QMHA_HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     std::lock_guard<std::mutex> lk(g_side_mu);
-    SideStream& ss = g_side[{dev, (void*)stream}];
+    SideStream& ss = g_side[{dev, (void*)stream, stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id()}];
     if (!ss.s) {
         QMHA_HIP_TRY(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking), "hipStreamCreate");
         QMHA_HIP_TRY(hipEventCreateWithFlags(&ss.start, hipEventDisableTiming), "hipEventCreate");
@@ -193,42 +154,95 @@ int get_side(hipStream_t stream, int nchunks, SideStream** out) {
 }
 
 // ---- library-owned workspaces, one per (device, stream) --------------------------------
+// Threading contract: any number of host threads may call every entry point at once.
+// The reference gets that from per-call cudaMalloc'd scratch and private streams (include/launchers.h:
+// 27-33, freed at :64-71); here the scratch is cached, so a call LEASES its (device, stream) slot: the
+// slot's mutex is held from the moment the buffer is handed out until the call's last kernel that uses
+// it has been enqueued.  Calls on one stream therefore enqueue one whole call after another (pre-pass and
+// main kernel of a call are never separated by another call's pre-pass), and the stream runs them in that
+// order.  Calls on different streams use different slots.  hipStreamPerThread names a different stream
+// in every thread, so its slot key carries the thread id.  A slot that must grow never frees the buffer
+// other enqueued work may still read: the old buffer is retired behind an event recorded on the slot's
+// stream and freed once that event has completed (checked at the slot's next lease, or at release).
 struct WsKey {
     int dev;
     void* stream;
-    bool operator<(const WsKey& o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
+    std::thread::id tid;  // hipStreamPerThread only
+    bool operator<(const WsKey& o) const {
+        if (dev != o.dev) return dev < o.dev;
+        if (stream != o.stream) return stream < o.stream;
+        return tid < o.tid;
+    }
 };
-struct WsBuf {
+struct WsSlot {
+    std::mutex lease;  // held across a call's enqueue
     void* ptr = nullptr;
     size_t bytes = 0;
+    std::vector<std::pair<void*, hipEvent_t>> retired;  // grown-out buffers, freed once their event completed
 };
-std::mutex g_ws_mu;
-std::map<WsKey, WsBuf> g_ws;
+std::mutex g_ws_mu;  // guards the map only (slots are never erased while the library is in use)
+std::map<WsKey, std::unique_ptr<WsSlot>> g_ws;
 
-int get_workspace(size_t need, hipStream_t stream, void** out) {
-    *out = nullptr;
-    if (need == 0) return QMHA_OK;
+// free the retired buffers whose last reader has completed (all when `wait`); caller holds the lease
+void reap_retired(WsSlot& s, bool wait) {
+    auto it = s.retired.begin();
+    while (it != s.retired.end()) {
+        if (wait) (void)hipEventSynchronize(it->second);
+        else if (hipEventQuery(it->second) != hipSuccess) {
+            ++it;
+            continue;
+        }
+        (void)hipEventDestroy(it->second);
+        (void)hipFree(it->first);
+        it = s.retired.erase(it);
+    }
+}
+
+// A held workspace: the buffer stays this call's until the lease is destroyed (after the last enqueue).
+struct WsLease {
+    std::unique_lock<std::mutex> lk;
+    void* ptr = nullptr;
+};
+
+int lease_workspace(size_t need, hipStream_t stream, WsLease* out) {
+    out->ptr = nullptr;
     int dev = 0;
     QMHA_HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    WsBuf& b = g_ws[WsKey{dev, (void*)stream}];
-    if (b.bytes < need) {
-        if (b.ptr) {
-            // the old buffer may still be read by work queued on this stream
-            QMHA_HIP_TRY(hipStreamSynchronize(stream), "hipStreamSynchronize");
-            (void)hipFree(b.ptr);
-            b.ptr = nullptr;
-            b.bytes = 0;
+    WsSlot* slot;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        const WsKey key{dev, (void*)stream, stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id()};
+        std::unique_ptr<WsSlot>& sp = g_ws[key];
+        if (!sp) sp.reset(new WsSlot);
+        slot = sp.get();
+    }
+    out->lk = std::unique_lock<std::mutex>(slot->lease);
+    WsSlot& s = *slot;
+    if (!s.retired.empty()) reap_retired(s, false);
+    if (need == 0) return QMHA_OK;
+    if (s.bytes < need) {
+        if (s.ptr) {
+            // work already enqueued on this stream may still read the old buffer: retire it behind an event
+            hipEvent_t ev = nullptr;
+            QMHA_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            const hipError_t e = hipEventRecord(ev, stream);
+            if (e != hipSuccess) {
+                (void)hipEventDestroy(ev);
+                return hip_fail(e, "hipEventRecord");
+            }
+            s.retired.emplace_back(s.ptr, ev);
+            s.ptr = nullptr;
+            s.bytes = 0;
         }
-        size_t alloc = qmha::align_up(need + need / 8, 1 << 20);
-        if (hipMalloc(&b.ptr, alloc) != hipSuccess) {
-            b.ptr = nullptr;
+        const size_t alloc = qmha::align_up(need + need / 8, 1 << 20);
+        if (hipMalloc(&s.ptr, alloc) != hipSuccess) {
+            s.ptr = nullptr;
             g_last_error = "hipMalloc of workspace failed";
             return QMHA_ERR_NOMEM;
         }
-        b.bytes = alloc;
+        s.bytes = alloc;
     }
-    *out = b.ptr;
+    out->ptr = s.ptr;
     return QMHA_OK;
 }
 
@@ -287,22 +301,9 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
         if (_st != QMHA_OK) return _st;                \
     } while (0)
 
-    const int nc0 = (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) ? overlap_chunks(B) : 1;
-    if (variant == QMHA_FA_TC_INT8_B && nc0 == 1 && qmha::int8_fused_on(D, N)) {
-        // one kernel quantises K / V and sweeps (FL_FUSED); its flag zeroing is part of it
-        QMHA_MARK(rec.main, stream, true);
-        QMHA_HIP_TRY(qmha::launch_fa_int8_fused(qmha::int8_carve(ws, B, N, h, D), Q, K, V, O, B, N, h, D, d_model, stream),
-                     "fa_int8 fused launch");
-        QMHA_MARK(rec.main, stream, false);
-    } else if (variant == QMHA_FA_TC_V1A && nc0 == 1 && qmha::f16_fused_on(D, N)) {
-        // one kernel converts K / V and sweeps (F16_FUSED); its flag zeroing is part of it
-        QMHA_MARK(rec.main, stream, true);
-        QMHA_HIP_TRY(qmha::launch_fa_f16_fused(qmha::f16_carve(ws, B, N, h, D), Q, K, V, O, B, N, h, D, d_model, stream),
-                     "fa_f16 fused launch");
-        QMHA_MARK(rec.main, stream, false);
-    } else if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
+    if (variant == QMHA_FA_TC_INT8_B || variant == QMHA_FA_TC_V1A) {
         const size_t slab = (size_t)N * d_model;  // floats per sequence
-        const int nc = nc0;
+        const int nc = overlap_chunks(B);
         SideStream* side = nullptr;
         if (nc > 1) {
             int st = get_side(stream, nc, &side);
@@ -319,7 +320,7 @@ int run(const float* Q, const float* K, const float* V, float* O, int B, int N, 
             QMHA_MARK(rec.pre, pre_s, true);
             if (variant == QMHA_FA_TC_INT8_B) {
                 const qmha::Int8Workspace w = int8_slice(w8, b0, N, h, D);
-                QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, qmha::int8_v_mode(D, N), nb, N, h, D,
+                QMHA_HIP_TRY(qmha::launch_quant_int8(Q + b0 * slab, K + b0 * slab, V + b0 * slab, w, w.Vh, /*v_mode=*/1, nb, N, h, D,
                                                      d_model, pre_s, /*first_tensor=*/1), "quant_int8 launch");
             } else {
                 QMHA_HIP_TRY(qmha::launch_convert_f16(Q + b0 * slab, K + b0 * slab, V + b0 * slab, f16_slice(w16, b0, N, h, D),
@@ -409,10 +410,10 @@ int qmha_solve_ex(const float* Q, const float* K, const float* V, float* O, int 
     int st = check_shape(Q, K, V, O, B, N, d_model, h, variant, &D);
     if (st != QMHA_OK) return st;
     const size_t need = workspace_bytes(B, N, h, D, variant);
-    void* ws = nullptr;
-    st = get_workspace(need, (hipStream_t)stream, &ws);
+    WsLease ws;  // held until every kernel of this call is enqueued
+    st = lease_workspace(need, (hipStream_t)stream, &ws);
     if (st != QMHA_OK) return st;
-    return run(Q, K, V, O, B, N, d_model, h, variant, ws, need, (hipStream_t)stream);
+    return run(Q, K, V, O, B, N, d_model, h, variant, ws.ptr, need, (hipStream_t)stream);
 }
 
 size_t qmha_workspace_size(int B, int N, int d_model, int h, int variant) {
@@ -422,14 +423,13 @@ size_t qmha_workspace_size(int B, int N, int d_model, int h, int variant) {
 
 int qmha_solve_variant(const float* Q, const float* K, const float* V, float* O, int N, int d_model, int h,
                        int variant) {
-    // blocking like the reference (launchers.h:64).  r04 A/B: polling hipStreamQuery on the null stream
-    // (2.01 ms per 16 calls at C4) or on a library-owned stream (2.06 ms) was slower than
-    // hipStreamSynchronize (1.94 ms, profiles/r04/ab_sync/summary.txt); r05: a stream-ordered host-flag
-    // write spun on (wait_null_stream) against hipStreamSynchronize, same box: 1.868 vs 1.883 ms per 16 C4
-    // calls, fp16 1.897 vs 1.919 ms (profiles/r05/ab_solve_sync/)
+    // blocking like the reference (launchers.h:64): hipStreamSynchronize.  r04 A/B: polling
+    // hipStreamQuery was slower (profiles/r04/ab_sync/summary.txt); r05's spin on a stream-ordered host
+    // flag saved ~1 us per call (profiles/r05/ab_solve_sync/) but pinned a host word per thread and a CPU
+    // core per waiting thread, so r06 returned to the runtime's synchronisation (round-5 ADVICE)
     int st = qmha_solve_ex(Q, K, V, O, 1, N, d_model, h, variant, nullptr);
     if (st != QMHA_OK) return st;
-    QMHA_HIP_TRY(wait_null_stream(), "solve: waiting for the null stream");
+    QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "solve: hipStreamSynchronize");
     return QMHA_OK;
 }
 
@@ -448,13 +448,13 @@ int qmha_quantize_int8(const float* X, int B, int N, int d_model, int h, int8_t*
     }
     if (layout == 2) {  // per-tensor (head-slice) scales: the single-read pass (slice counters in a workspace)
         const size_t need = qmha::align_up((size_t)6 * B * h * sizeof(uint32_t), 256);
-        void* ws = nullptr;
-        st = get_workspace(need, (hipStream_t)stream, &ws);
+        WsLease ws;  // held until the pass is enqueued
+        st = lease_workspace(need, (hipStream_t)stream, &ws);
         if (st != QMHA_OK) return st;
         qmha::Int8Workspace w{};
         w.Ki = Xi;  // the K role: int8 rows
         w.sK = scales;
-        w.slice_sync = static_cast<uint32_t*>(ws);
+        w.slice_sync = static_cast<uint32_t*>(ws.ptr);
         QMHA_HIP_TRY(qmha::launch_quant_int8_pt_rows(X, w, B, N, h, D, d_model, (hipStream_t)stream), "quant_int8_pt launch");
         return QMHA_OK;
     }
@@ -486,12 +486,14 @@ int qmha_debug_qk_int32(const float* Q, const float* K, int N, int d_model, int 
         return QMHA_ERR_INVALID;
     }
     const size_t need = qmha::int8_workspace_bytes(1, N, h, D, /*with_q=*/true);
-    void* ws = nullptr;
-    st = get_workspace(need, nullptr, &ws);
+    WsLease lease;
+    st = lease_workspace(need, nullptr, &lease);
     if (st != QMHA_OK) return st;
+    void* ws = lease.ptr;
     qmha::Int8Workspace w = qmha::int8_carve(ws, 1, N, h, D, /*with_q=*/true);
     QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, Q, w, w.Vh, 1, 1, N, h, D, d_model, nullptr), "quant_int8 launch");
     QMHA_HIP_TRY(qmha::launch_debug_qk_int32(w, N, D, head, S, nullptr), "debug_qk launch");
+    lease.lk.unlock();
     QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
     return QMHA_OK;
 }
@@ -506,14 +508,16 @@ int qmha_debug_fa_int8_dump(const float* Q, const float* K, const float* V, floa
         return QMHA_ERR_INVALID;
     }
     const size_t need = qmha::int8_workspace_bytes(B, N, h, D);
-    void* ws = nullptr;
-    st = get_workspace(need, nullptr, &ws);
+    WsLease lease;
+    st = lease_workspace(need, nullptr, &lease);
     if (st != QMHA_OK) return st;
+    void* ws = lease.ptr;
     const qmha::Int8Workspace w = qmha::int8_carve(ws, B, N, h, D);
-    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, qmha::int8_v_mode(D, N), B, N, h, D, d_model, nullptr, /*first_tensor=*/1),
+    QMHA_HIP_TRY(qmha::launch_quant_int8(Q, K, V, w, w.Vh, /*v_mode=*/1, B, N, h, D, d_model, nullptr, /*first_tensor=*/1),
                  "quant_int8 launch");
     QMHA_HIP_TRY(qmha::launch_fa_int8_dump(w, Q, O, B, N, h, D, d_model, qmha::QkDump{S, Qi, sQ}, nullptr),
                  "fa_int8 dump launch");
+    lease.lk.unlock();
     QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
     return QMHA_OK;
 }
@@ -528,13 +532,15 @@ int qmha_debug_fa_int8_pt_dump(const float* Q, const float* K, const float* V, f
         return QMHA_ERR_INVALID;
     }
     const size_t need = qmha::int8_pt_workspace_bytes(B, N, h, D);
-    void* ws = nullptr;
-    st = get_workspace(need, nullptr, &ws);
+    WsLease lease;
+    st = lease_workspace(need, nullptr, &lease);
     if (st != QMHA_OK) return st;
+    void* ws = lease.ptr;
     const qmha::Int8Workspace w = qmha::int8_pt_carve(ws, B, N, h, D);
     QMHA_HIP_TRY(qmha::launch_quant_int8_pt(Q, K, V, w, B, N, h, D, d_model, nullptr), "quant_int8_pt launch");
     QMHA_HIP_TRY(qmha::launch_fa_int8_pt_dump(w, Q, O, B, N, h, D, d_model, qmha::QkDump{S, Qi, sQ}, nullptr),
                  "fa_int8_pt dump launch");
+    lease.lk.unlock();
     QMHA_HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
     return QMHA_OK;
 }
@@ -578,10 +584,6 @@ const char* qmha_version(void) { return QMHA_VERSION_STRING; }
 const char* qmha_last_error(void) { return g_last_error.c_str(); }
 
 int64_t qmha_debug_set_pt_wait(int64_t ticks) { return qmha::set_pt_wait_ticks(ticks); }
-int qmha_debug_set_int8_fused(int mode) { return qmha::set_int8_fused(mode); }
-int64_t qmha_debug_set_int8_fused_wait(int64_t ticks) { return qmha::set_int8_fused_wait(ticks); }
-int qmha_debug_set_int8_fused_ablate(int bits) { return qmha::set_int8_fused_ablate(bits); }
-int qmha_debug_set_f16_fused(int mode) { return qmha::set_f16_fused(mode); }
 
 int qmha_set_overlap_chunks(int n) {
     const int prev = overlap_chunks(1 << 30);
@@ -637,14 +639,18 @@ void qmha_release_workspaces(void) {
         }
         g_side.clear();
     }
+    // each slot under its lease: a call still enqueueing on it finishes first; the buffers are freed
+    // after the device has drained (work on any stream may still read them)
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (auto& kv : g_ws) {
-        if (kv.second.ptr) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(kv.second.ptr);
-        }
+        WsSlot& s = *kv.second;
+        std::lock_guard<std::mutex> lease(s.lease);
+        (void)hipDeviceSynchronize();
+        reap_retired(s, true);
+        if (s.ptr) (void)hipFree(s.ptr);
+        s.ptr = nullptr;
+        s.bytes = 0;
     }
-    g_ws.clear();
 }
 
 #ifndef QMHA_NO_DEFAULT_SOLVE

@@ -243,8 +243,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // (tools/lds_banks.py models both sides; the 8-byte read-back stays at its 2-way floor).
 constexpr int QMHA_VT_PITCH = 64 + 8;  // bytes per d-row of the LDS tile (8-byte pad)
 __device__ __forceinline__ int vt_chunk_swz(int d) { return (d >> 4) & 7; }
-// COH: the lines are stored as agent-coherent 8-byte stores (sc1: visible to the other XCDs once
-// the wave's stores have completed), for a consumer inside the same launch (the fused int8 kernel)
 // The two halves of vt_group_store: vt_tile_write puts hf(a, c) -- this lane's four f16 values of column
 // 4 c4 + c, kv rows NI rq + 4a .. +3 (one 8-byte chunk) -- into the wave's LDS tile; vt_tile_store reads the
 // tile back as 16-byte lines and stores them to dst (a caller may rewrite the tile in between).
@@ -262,7 +260,7 @@ __device__ __forceinline__ void vt_tile_write(char* T, int lane, HF&& hf) {
         }
     }
 }
-template <int D, bool COH = false>
+template <int D>
 __device__ __forceinline__ void vt_tile_store(const char* T, int lane, char* dst) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
@@ -272,16 +270,10 @@ __device__ __forceinline__ void vt_tile_store(const char* T, int lane, char* dst
         const int d = u >> 2, q = u & 3;
         const v2i lo = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q) ^ vt_chunk_swz(d)));
         const v2i hi = *reinterpret_cast<const v2i*>(T + d * QMHA_VT_PITCH + 8 * ((2 * q + 1) ^ vt_chunk_swz(d)));
-        if constexpr (COH) {
-            uint64_t* p = reinterpret_cast<uint64_t*>(dst + 16 * u);
-            __hip_atomic_store(p, __builtin_bit_cast(uint64_t, lo), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(p + 1, __builtin_bit_cast(uint64_t, hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
-        }
+        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{lo[0], lo[1], hi[0], hi[1]};
     }
 }
-template <int D, bool QUANT, bool COH = false>
+template <int D, bool QUANT>
 __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
     vt_tile_write<D>(T, lane, [&](int a, int c) {
         v4h h;
@@ -289,15 +281,14 @@ __device__ __forceinline__ void vt_group_store(char* T, const v4f (&x)[D / 8], f
         for (int e = 0; e < 4; ++e) h[e] = QUANT ? (_Float16)qmha_quant_i8(x[4 * a + e][c], inv) : (_Float16)x[4 * a + e][c];
         return h;
     });
-    vt_tile_store<D, COH>(T, lane, dst);
+    vt_tile_store<D>(T, lane, dst);
 }
 
 // The same for the int8 V^T operand ([D][32 slots] bytes, kv_of_slot_i8 order; the standalone
 // qmha_quantize_int8 layout 1): four consecutive kv rows are four consecutive slots, so a lane
 // packs its 4-row runs of one column into one dword (ds_write_b32 instead of byte stores).
 constexpr int QMHA_VT8_PITCH = 32 + 4;  // bytes per d-row of the int8 LDS tile
-// COH: agent-coherent 8-byte stores (the fused int8 kernel's producers under FL_I8PV)
-template <int D, bool COH = false>
+template <int D>
 __device__ __forceinline__ void vt8_group_store(char* T, const v4f (&x)[D / 8], float inv, int lane, char* dst) {
     constexpr int C4 = D / 4, NI = D / 8;
     const int rq = lane / C4, c4 = lane % C4;
@@ -319,12 +310,6 @@ __device__ __forceinline__ void vt8_group_store(char* T, const v4f (&x)[D / 8], 
     for (int u = lane; u < LINES; u += 64) {
         const int d = u >> 1, q = u & 1;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(T + d * QMHA_VT8_PITCH + 16 * q);
-        if constexpr (COH) {
-            uint64_t* p = reinterpret_cast<uint64_t*>(dst + 16 * u);
-            __hip_atomic_store(p, (uint64_t)r[0] | ((uint64_t)r[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(p + 1, (uint64_t)r[2] | ((uint64_t)r[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{(int)r[0], (int)r[1], (int)r[2], (int)r[3]};
-        }
+        *reinterpret_cast<v4i*>(dst + 16 * u) = v4i{(int)r[0], (int)r[1], (int)r[2], (int)r[3]};
     }
 }

@@ -12,10 +12,8 @@
 // v_mfma_f32_32x32x16_f16 with swapped operands.  The O accumulator is the MFMA C operand,
 // so the P@V accumulation costs no VALU; alpha == 1 rescales are skipped exactly.
 #include "qmha_common.hpp"
-#include "qmha_fused.hpp"
 #include "qmha_kernels.hpp"
 
-#include <atomic>
 #include <type_traits>
 
 namespace qmha {
@@ -33,51 +31,14 @@ static constexpr float kLog2eH = 1.4426950408889634f;
 // F16_UNROLL: two stages per loop trip, so each stage's LDS buffer is a compile-time constant and
 // every operand read is a base register plus an immediate (no per-tile address arithmetic)
 // F16_LB1: a one-wave-per-SIMD register budget (VGPRs + AGPRs) for d > 128, whose O alone is d/2 VGPRs
-// F16_FUSED: the K / V conversion pre-pass done by the kernel's own workgroups (qmha_fused.hpp): one launch
-// per call (plus a flag-zeroing one) instead of two
-enum { F16_PREFETCH = 1, F16_STAMP = 2, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16, F16_LB1 = 32, F16_FUSED = 64 };
-
-struct FusedF16 {
-    const float* K;  // the caller's fp32 K, V  [B][N][d_model]
-    const float* V;
-    _Float16* Kh;    // the kernel's f16 K rows / V^T operand (what it streams from)
-    _Float16* Vt;
-    FusedCtl ctl;
-};
-
-// One wave converts K group g and V group g of head slice bh (fa_tc_v1a.cu:300-330: __float2half, RNE -- the
-// pre-pass qmha_convert_f16_kernel's arithmetic and layouts) with agent-coherent stores, then flags it.
-template <int D>
-__device__ __forceinline__ void produce_f16_group(const FusedF16& f, int bh, int g, int H, int N, int G, int d_model,
-                                                  int lane, char* T) {
-    constexpr int C4 = D / 4, RPI = 64 / C4, NK = 32 / RPI, NV = D / 8;
-    const int b = bh / H, k = bh % H;
-    const int ri = lane / C4, ci = lane % C4;
-    const size_t base = ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-    v4f kx[NK], vx[NV];
-#pragma unroll
-    for (int i = 0; i < NK; ++i)  // K: rows i * RPI + ri
-        kx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.K + base + (size_t)(i * RPI + ri) * d_model));
-#pragma unroll
-    for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
-        vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
-    _Float16* kd = f.Kh + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-#pragma unroll
-    for (int i = 0; i < NK; ++i) {
-        v4h h;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) h[c] = (_Float16)kx[i][c];  // RNE (= __float2half)
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(kd + (size_t)(i * RPI + ri) * D), __builtin_bit_cast(uint64_t, h),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    vt_group_store<D, false, true>(T, vx, 1.0f, lane, reinterpret_cast<char*>(f.Vt + ((size_t)bh * G + g) * (size_t)(32 * D)));
-    fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
-}
+// (Measured and not shipped, in git history up to commit df5dced: the K / V conversion inside the sweep,
+// F16_FUSED; the per-phase s_memtime stamps, F16_STAMP.)
+enum { F16_PREFETCH = 1, F16_LB4 = 4, F16_VPRE = 8, F16_UNROLL = 16, F16_LB1 = 32 };
 
 template <int D, int WAVES, int SG, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 1 : 2)) void qmha_fa_f16_v2_kernel(
     const float* __restrict__ Qf, const _Float16* __restrict__ Kh, const _Float16* __restrict__ Vt,
-    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, FusedF16 fz = FusedF16{}) {
+    float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2) {
     QMHA_ENABLE_AGPR_MFMA();
     // the score scale lives in a VGPR: a VOP3 fma reading an SGPR issues at the slow rate
     // (~4.3 instead of ~2.5 cycles per wave64 on gfx950, profiles/r02/ubench_valu_cost.txt)
@@ -89,11 +50,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
     constexpr int VBYTES = SG * 32 * D * 2;
     constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
     static_assert(KCH % 64 == 0 && VCH % 64 == 0 && (KCH / SG) % 64 == 0, "whole KiB LDS-DMA pieces");
-    constexpr bool FUSED = FL & F16_FUSED;
-    // F16_FUSED: the producers' per-wave V^T transpose tiles live in the stage buffers before the first DMA
-    constexpr int SB0 = KBYTES + VBYTES, TB = FUSED ? WAVES * D * QMHA_VT_PITCH : 0;
-    constexpr int SB = 2 * SB0 >= TB ? SB0 : (TB + 31) / 32 * 16;
-    __shared__ __attribute__((aligned(16))) char lds[2][SB];
+    __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
 
     const int G = N / QMHA_GROUP;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -104,12 +61,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
     const int qg = qb * WAVES + wave;
     const bool active = qg < G;
     const int half = lane >> 5, col = lane & 31;
-    if constexpr (FUSED) {
-        char* T = &lds[0][0] + wave * (D * QMHA_VT_PITCH);
-        fused_produce_and_wait<WAVES>(fz.ctl, wg, bh, nqb, G, wave, lane, [&](int pbh, int pg) {
-            produce_f16_group<D>(fz, pbh, pg, H, N, G, d_model, lane, T);
-        });
-    }
 
     v8h qop[KS];
     if (active) {
@@ -135,31 +86,23 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
 #pragma unroll
     for (int m = 0; m < MB; ++m) o[m] = v16f{};
     float m_run = 0.0f, l_run = 0.0f;  // m0 = 0 (fa_tc_v1a.cu:290); l_run per lane half
-    unsigned long long stamp[4] = {0, 0, 0, 0};  // F16_STAMP diagnostics only
-    const unsigned long long k_t0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
-    const unsigned long long k_r0 = (FL & F16_STAMP) ? __builtin_amdgcn_s_memrealtime() : 0;
 
     const char* kbase = reinterpret_cast<const char*>(Kh + (size_t)bh * N * D);
     const char* vbase = reinterpret_cast<const char*>(Vt + (size_t)bh * N * D);
-    // F16_FUSED: written by this launch -- no load through them may move above the wait
-    if constexpr (FUSED) asm volatile("" : "+s"(kbase), "+s"(vbase));
     const int nst = (G + SG - 1) / SG;
 
     // stages arrive by buffer_load ... lds: fixed per-lane source offsets, the stage offset in soffset
     constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
     int koff[KJ], voff[VJ];
-    // F16_FUSED: offsets from a lane id the compiler cannot hoist above the production (qmha_fa_int8.hip)
-    int lane_o = lane;
-    if constexpr (FUSED) asm volatile("" : "+v"(lane_o));
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane_o;
+        const int idx = (wave + jj * WAVES) * 64 + lane;
         const int row = idx / (RB / 16), cc = swz_src<RB>(row, idx % (RB / 16));
         koff[jj] = row * RB + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane_o;
+        const int idx = (wave + jj * WAVES) * 64 + lane;
         const int grp = idx / (4 * D), w = idx % (4 * D);
         const int d = w >> 2, cv = swz_src<64>(d, w & 3);
         voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
@@ -281,35 +224,11 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
                     __builtin_amdgcn_sched_barrier(0);
                     s_cur = s_nxt;
                 }
-            } else if constexpr (FL & F16_STAMP) {
-                for (int gi = 0; gi < ngr; ++gi) {
-                    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-                    v16f s = qk(L, gi);
-                    asm volatile("" : "+v"(s));
-                    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-                    const float x = s[0] + s[7] + s[15];  // forces the QK result
-                    asm volatile("" :: "v"(x));
-                    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-                    tile(L, gi, s);
-                    asm volatile("" : "+v"(o[0]));
-                    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-                    stamp[0] += t1 - t0;
-                    stamp[1] += t2 - t1;
-                    stamp[2] += t3 - t2;
-                }
             } else {
                 for (int gi = 0; gi < ngr; ++gi) tile(L, gi, qk(L, gi));
             }
         }
-        const unsigned long long tb = (FL & F16_STAMP) ? __builtin_amdgcn_s_memtime() : 0;
         qmha_dma_barrier();
-        if constexpr (FL & F16_STAMP) stamp[3] += __builtin_amdgcn_s_memtime() - tb;
-    }
-    if constexpr (FL & F16_STAMP) {
-        if (lane == 0 && (blockIdx.x % 997) == 0)
-            printf("stamp wg %d wave %d: qk_issue %llu qk_wait %llu tile %llu barrier %llu (tiles %d) total %llu real100MHz %llu\n",
-                   (int)blockIdx.x, wave, stamp[0], stamp[1], stamp[2], stamp[3], G,
-                   __builtin_amdgcn_s_memtime() - k_t0, __builtin_amdgcn_s_memrealtime() - k_r0);
     }
     if (active) {
         l_run = half_swap_add(l_run);
@@ -327,10 +246,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
     }
 }
 
-// Kh, Vt (Q is converted in the main kernel), then the fused kernel's group flags [B*H][N/32]
-size_t f16_workspace_bytes(int B, int N, int H, int D) {
-    return 2 * align_up((size_t)B * H * N * D * 2, 256) + align_up((size_t)B * H * (N / QMHA_GROUP) * 4, 256);
-}
+// Kh, Vt (Q is converted in the main kernel)
+size_t f16_workspace_bytes(int B, int N, int H, int D) { return 2 * align_up((size_t)B * H * N * D * 2, 256); }
 
 F16Workspace f16_carve(void* ws, int B, int N, int H, int D) {
     const size_t e = align_up((size_t)B * H * N * D * 2, 256);
@@ -339,7 +256,6 @@ F16Workspace f16_carve(void* ws, int B, int N, int H, int D) {
     w.Qh = nullptr;
     w.Kh = reinterpret_cast<_Float16*>(p);
     w.Vt = reinterpret_cast<_Float16*>(p + e);
-    w.kv_ready = reinterpret_cast<uint32_t*>(p + 2 * e);
     return w;
 }
 
@@ -350,7 +266,7 @@ static hipError_t fa_f16_v2_launch(const F16Workspace& w, const float* Qf, float
     const int nqb = (G + WAVES - 1) / WAVES;
     const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;
     hipLaunchKernelGGL((qmha_fa_f16_v2_kernel<D, WAVES, SG, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
-                       w.Kh, w.Vt, O, N, H, d_model, nqb, c_log2, FusedF16{});
+                       w.Kh, w.Vt, O, N, H, d_model, nqb, c_log2);
     return hipGetLastError();
 }
 
@@ -372,8 +288,6 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
             case 441: return fa_f16_v2_launch<D, 4, 4, F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 424: return fa_f16_v2_launch<D, 4, 2, F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
             case 425: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
-            case 426: return fa_f16_v2_launch<D, 4, 2, F16_STAMP | F16_LB4>(w, Qf, O, B, N, H, d_model, stream);
-            case 422: return fa_f16_v2_launch<D, 4, 2, F16_STAMP>(w, Qf, O, B, N, H, d_model, stream);
             case 427: return fa_f16_v2_launch<D, 4, 2, F16_LB4 | F16_VPRE | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
             case 447: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE>(w, Qf, O, B, N, H, d_model, stream);
             case 448: return fa_f16_v2_launch<D, 4, 4, F16_LB4 | F16_VPRE | F16_PREFETCH>(w, Qf, O, B, N, H, d_model, stream);
@@ -398,57 +312,6 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
         return fa_f16_v2_launch<D, (D <= 64 ? QMHA_F16_WAVES : 4), 2, QMHA_F16_FL>(w, Qf, O, B, N, H, d_model, stream);
     else
         return fa_f16_v2_launch<D, 4, 2, F16_UNROLL | (D > 128 ? F16_LB1 : 0)>(w, Qf, O, B, N, H, d_model, stream);
-}
-
-// ---- F16_FUSED launch: zero the group flags, then the main kernel that converts K / V itself
-static std::atomic<int> g_f16_fused_mode{0};  // 0 two launches (default), 1 fused, 2 fused + cross-XCD test rule
-int set_f16_fused(int mode) { return g_f16_fused_mode.exchange(mode); }
-bool f16_fused_on(int D, int N) { return g_f16_fused_mode.load() != 0 && (D == 32 || D == 64 || D == 128) && N >= QMHA_GROUP; }
-
-template <int D, int WAVES, int SG, int FL>
-static hipError_t fa_f16_fused_launch(const F16Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O,
-                                      int B, int N, int H, int d_model, hipStream_t stream) {
-    constexpr int FLF = FL | F16_FUSED;
-    const int G = N / QMHA_GROUP;
-    const int nqb = (G + WAVES - 1) / WAVES;
-    const long long nwg = (long long)B * H * nqb;
-    // resident workgroups per XCD (HIP's occupancy answer x CUs / 8), cached per device; 0 if unknown
-    static std::atomic<int> r_of[64];
-    int dev = 0, R = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        R = r_of[dev].load(std::memory_order_relaxed);
-        if (R <= 0) {
-            int occ = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qmha_fa_f16_v2_kernel<D, WAVES, SG, FLF>, WAVES * 64, 0) ==
-                    hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ > 0 && cus > 0) {
-                R = occ * cus / 8;
-                r_of[dev].store(R, std::memory_order_relaxed);
-            }
-        }
-    }
-    if (R <= 0 || nqb > R || nwg > INT32_MAX) {  // occupancy unknown or a head longer than a round: two launches
-        hipError_t e = launch_convert_f16(Qf, Kf, Vf, w, B, N, H, D, d_model, stream);
-        return e != hipSuccess ? e : fa_f16_v2_launch<D, WAVES, SG, FL>(w, Qf, O, B, N, H, d_model, stream);
-    }
-    hipError_t e = launch_zero_u32(w.kv_ready, B * H * G, stream);
-    if (e != hipSuccess) return e;
-    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2eH;
-    const FusedF16 fz{Kf, Vf, w.Kh, w.Vt, FusedCtl{w.kv_ready, R, g_f16_fused_mode.load() == 2 ? 1 : 0, 5000, 0}};
-    hipLaunchKernelGGL((qmha_fa_f16_v2_kernel<D, WAVES, SG, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Kh,
-                       w.Vt, O, N, H, d_model, nqb, c_log2, fz);
-    return hipGetLastError();
-}
-
-hipError_t launch_fa_f16_fused(const F16Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
-                               int N, int H, int D, int d_model, hipStream_t stream) {
-    if (!f16_fused_on(D, N) || !w.kv_ready) return hipErrorInvalidValue;
-    switch (D) {
-        case 32: return fa_f16_fused_launch<32, QMHA_F16_WAVES, 2, QMHA_F16_FL>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 64: return fa_f16_fused_launch<64, QMHA_F16_WAVES, 2, QMHA_F16_FL>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 128: return fa_f16_fused_launch<128, 4, 2, QMHA_F16_FL>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,

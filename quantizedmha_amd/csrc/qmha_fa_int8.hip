@@ -34,15 +34,10 @@
 // timeline) were kept in tools/ablation/qmha_fa_int8_ablation.hip until round 5 (git history, up to
 // commit 6d5deec); DESIGN.md cites their measurements.
 #include "qmha_common.hpp"
-#include "qmha_fused.hpp"
 #include "qmha_kernels.hpp"
 
 #include <atomic>
 #include <type_traits>
-
-#ifndef QMHA_FOLD_PK
-#define QMHA_FOLD_PK 0  // A/B builds: -DQMHA_FOLD_PK=1, the per-block O fold as packed fp32 fmas
-#endif
 
 namespace qmha {
 
@@ -106,15 +101,10 @@ __device__ __forceinline__ float quant_q_operand(const float* __restrict__ row, 
 //             removed), its in-register Q operand and sQ (qmha_debug_fa_int8_dump: the bit-exact
 //             check of the production Q@K^T path; never the production launch)
 //   FL_PT     (pipe kernel) the per-tensor mode fa_tc_int8_pt
-//   FL_FUSED  (pipe kernel, per-block mode) the K/V pre-pass done by the kernel's own workgroups
-//             (FusedKV below): one launch per call instead of two
-//   FL_I8PV   (pipe kernel, per-block mode) P@V on v_mfma_i32_32x32x32_i8: V staged as int8 in the i8
-//             V^T operand order (half the bytes), P packed to bytes, the int32 result read off its
-//             magic-biased accumulator; bit-identical to the f16 form (see the kernel)
-enum {
-    FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576,
-    FL_FUSED = 2097152, FL_I8PV = 4194304
-};
+// Measured and not shipped (the sources are in git history up to commit df5dced):
+// the K/V pre-pass inside the sweep (FL_FUSED), P@V on the i8 matrix core per block (FL_I8PV) and per
+// tensor (FL_PT | FL_I8PV), the fold as packed fmas (QMHA_FOLD_PK), 12-wave workgroups (QMHA_INT8_W64).
+enum { FL_MAGIC = 1, FL_LB1 = 2, FL_LB2 = 4, FL_JIT = 8, FL_LB4 = 16, FL_KFOLD = 64, FL_DUMP = 256, FL_PT = 1048576 };
 
 // ---------------------------------------------------------------------------------------
 // One-tile-at-a-time main kernel (every head size; N = 32).
@@ -367,203 +357,15 @@ __device__ __forceinline__ void pin_regs(float (&v)[N], int lo, int hi) {
         if (i >= lo && i < hi) asm volatile("" : "+v"(v[i]));
 }
 
-// ---------------------------------------------------------------------------------------
-// FL_FUSED (r04): the per-block K/V quantisation (fa_tc_int8_b.cu:33-152, the arithmetic of
-// qmha_prepass.hip quant_row_group / quant_v_group) done by the main kernel's own workgroups, so a
-// call is one launch (plus a flag-zeroing one) and the pre-pass's HBM traffic runs under the
-// VALU-bound sweep instead of before it.  Work split, flags and coherence: qmha_fused.hpp.  The
-// scales are padded to whole 128-byte lines per head (sstride), each read only after the whole head is
-// flagged.
-// ---------------------------------------------------------------------------------------
-struct FusedKV {
-    const float* K;        // the caller's fp32 K, V  [B][N][d_model]
-    const float* V;
-    int8_t* Ki;            // the kernel's K / V / scale arrays (what it streams from)
-    _Float16* Vh;
-    float* sK;             // [B*H][sstride]
-    float* sV;
-    int sstride;           // scales per head: G rounded up to 32
-    FusedCtl ctl;          // flags, residency, test mode, wait bound
-};
-
-// One wave quantises K group g and V group g of head slice bh and publishes them.
-//   Fast path (r05): absmax by v_max3 on |x|; Pi = rint(RN(x / s)) as the reference's __float2int_rn(x * inv)
-//   -- the product rounded first, then a magic add rounds it half-even to an integer held in the low
-//   bits (u = RN(x * inv) + 1.5 * 2^23, byte 0 of u = the int8), both as packed fp32 ops; K bytes
-//   packed by three v_perm per 4 values; V's f16 integers by one v_cvt_pkrtz per 2 values (exact:
-//   |Pi| <= 128).  No clamp is needed: |x * inv| <= 127 (1 + 2^-22) for finite inputs.  A NaN or an
-//   infinity anywhere in the group shows as a result outside [M - 128, M + 127] (checked by v_max3_u32
-//   on the bits), and that group takes the exact path below instead, before anything is stored.
-//   Exact path (r04; NaN -> 0, this unit is built with -fno-honor-nans): the IEEE pre-pass's fmaxf drops
-//   a NaN from the absmax and __float2int_rn maps it to 0, so the bytes are the same.
-// ablate (DESIGN.md 5.2d measurements only, qmha_debug_set_int8_fused_ablate; bits 0 and 2 in
-// qmha_fused.hpp): bit 1 plain stores and no completion wait before the flag; bit 3 the exact path for
-// every group.
-template <int D, bool V8 = false>  // V8: V as int8 in the i8 V^T operand order (FL_I8PV), exact quantiser
-__device__ __forceinline__ void produce_kv_group(const FusedKV& f, int bh, int g, int H, int N, int G, int d_model,
-                                                 int lane, char* T) {
-    constexpr int C4 = D / 4, RPI = 64 / C4, NK = 32 / RPI, NV = D / 8;
-    constexpr float M = QMHA_MAGIC_RNE;  // 1.5 * 2^23
-    const int b = bh / H, k = bh % H;
-    const int ri = lane / C4, ci = lane % C4;
-    const size_t base = ((size_t)b * N + (size_t)g * QMHA_GROUP) * d_model + (size_t)k * D + 4 * ci;
-    v4f kx[NK], vx[NV];
-#pragma unroll
-    for (int i = 0; i < NK; ++i)  // K: rows i * RPI + ri (quant_row_group's map)
-        kx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.K + base + (size_t)(i * RPI + ri) * d_model));
-    const bool coh = !(f.ctl.ablate & 2);
-    int8_t* kd = f.Ki + ((size_t)bh * N + (size_t)g * QMHA_GROUP) * D + 4 * ci;
-    char* vd = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(64 * D);
-    float* skp = f.sK + (size_t)bh * f.sstride + g;
-    float* svp = f.sV + (size_t)bh * f.sstride + g;
-    auto store_k = [&](uint32_t* p, uint32_t w) {
-        if (coh)
-            __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            *p = w;
-    };
-    auto store_scales = [&](float sk, float sv) {
-        if (lane == 0) {
-            store_k(reinterpret_cast<uint32_t*>(skp), __float_as_uint(sk));
-            store_k(reinterpret_cast<uint32_t*>(svp), __float_as_uint(sv));
-        }
-    };
-    const bool allow_fast = !(f.ctl.ablate & 8);
-    // u = RN(x * inv) + M, two at a time (v_pk_mul / v_pk_add, no contraction); hi = the largest bit pattern
-    // the magic constant as an opaque register value of the producer (no CSE with the sweep's own uses)
-    float Mv = M;
-    asm volatile("" : "+v"(Mv));
-    auto q2 = [&](float x0, float x1, float inv, uint32_t& hi) {
-#pragma clang fp contract(off)
-        const v2f u = v2f{x0, x1} * v2f{inv, inv} + v2f{Mv, Mv};
-        hi = max(hi, max(__float_as_uint(u[0]), __float_as_uint(u[1])));
-        return u;
-    };
-    constexpr uint32_t kHi = 0x4B40007Fu;  // bits of M + 127: finite groups stay at or below it
-    // ---- K: int8 rows, stored as they are made; a group with a NaN / infinity is redone exactly (its flag
-    // is set only at the end, so no consumer sees the first bytes)
-    float sk, sv;
-    auto k_exact = [&]() {
-        float ka = 0.0f;
-#pragma unroll
-        for (int i = 0; i < NK; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                kx[i][c] = nan_to_zero(kx[i][c]);
-                ka = fmaxf(ka, fabsf(kx[i][c]));
-            }
-        sk = qmha_scale_from_absmax(wave_max64(ka));
-        const float ik = 1.0f / sk;
-#pragma unroll
-        for (int i = 0; i < NK; ++i) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) w |= ((uint32_t)(uint8_t)qmha_quant_i8(kx[i][c], ik)) << (8 * c);
-            store_k(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), w);
-        }
-    };
-    if (allow_fast) {
-        float ka = 0.0f;
-#pragma unroll
-        for (int i = 0; i < NK; ++i)
-            ka = fmaxf(fmaxf(ka, fmaxf(fabsf(kx[i][0]), fabsf(kx[i][1]))), fmaxf(fabsf(kx[i][2]), fabsf(kx[i][3])));
-        sk = qmha_scale_from_absmax(wave_max64(ka));  // :104-106
-        const float ik = 1.0f / sk;
-        uint32_t hi = 0;
-#pragma unroll
-        for (int i = 0; i < NK; ++i) {
-            const v2f u01 = q2(kx[i][0], kx[i][1], ik, hi), u23 = q2(kx[i][2], kx[i][3], ik, hi);
-            const uint32_t t01 = __builtin_amdgcn_perm(__float_as_uint(u01[1]), __float_as_uint(u01[0]), 0x0c0c0400u);
-            const uint32_t t23 = __builtin_amdgcn_perm(__float_as_uint(u23[1]), __float_as_uint(u23[0]), 0x0c0c0400u);
-            store_k(reinterpret_cast<uint32_t*>(kd + (size_t)(i * RPI + ri) * D), __builtin_amdgcn_perm(t23, t01, 0x05040100u));
-        }
-        if (__builtin_amdgcn_ballot_w64(hi > kHi)) k_exact();
-    } else {
-        k_exact();
-    }
-    // ---- V: f16 integers in the V^T operand order, through the wave's LDS tile (rewritten exactly if needed)
-    if constexpr (V8) {  // FL_I8PV: int8 V^T, the pre-pass's exact arithmetic (quant_v_group, v_mode 0)
-#pragma unroll
-        for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt8_group_store's map)
-            vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
-        float va = 0.0f;
-#pragma unroll
-        for (int i = 0; i < NV; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                vx[i][c] = nan_to_zero(vx[i][c]);
-                va = fmaxf(va, fabsf(vx[i][c]));
-            }
-        sv = qmha_scale_from_absmax(wave_max64(va));
-        char* vd8 = reinterpret_cast<char*>(f.Vh) + ((size_t)bh * G + g) * (size_t)(32 * D);
-        if (coh)
-            vt8_group_store<D, true>(T, vx, 1.0f / sv, lane, vd8);
-        else
-            vt8_group_store<D, false>(T, vx, 1.0f / sv, lane, vd8);
-    } else {
-#pragma unroll
-        for (int i = 0; i < NV; ++i)  // V: rows NV * ri + i (vt_group_store's map)
-            vx[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(f.V + base + (size_t)(NV * ri + i) * d_model));
-        auto v_exact = [&]() {
-            float va = 0.0f;
-#pragma unroll
-            for (int i = 0; i < NV; ++i)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    vx[i][c] = nan_to_zero(vx[i][c]);
-                    va = fmaxf(va, fabsf(vx[i][c]));
-                }
-            sv = qmha_scale_from_absmax(wave_max64(va));
-            const float iv = 1.0f / sv;
-            vt_tile_write<D>(T, lane, [&](int a, int c) {
-                v4h h;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) h[e] = (_Float16)qmha_quant_i8(vx[4 * a + e][c], iv);
-                return h;
-            });
-        };
-        if (allow_fast) {
-            float va = 0.0f;
-#pragma unroll
-            for (int i = 0; i < NV; ++i)
-                va = fmaxf(fmaxf(va, fmaxf(fabsf(vx[i][0]), fabsf(vx[i][1]))), fmaxf(fabsf(vx[i][2]), fabsf(vx[i][3])));
-            sv = qmha_scale_from_absmax(wave_max64(va));
-            const float iv = 1.0f / sv;
-            uint32_t hi = 0;
-            vt_tile_write<D>(T, lane, [&](int a, int c) {  // rows 4a .. 4a + 3 of this lane's NV, column c
-                const v2f u01 = q2(vx[4 * a][c], vx[4 * a + 1][c], iv, hi);
-                const v2f u23 = q2(vx[4 * a + 2][c], vx[4 * a + 3][c], iv, hi);
-                const v2f y01 = u01 - v2f{Mv, Mv}, y23 = u23 - v2f{Mv, Mv};  // exact integers
-                const v2h h01 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y01[0], y01[1]));
-                const v2h h23 = __builtin_bit_cast(v2h, __builtin_amdgcn_cvt_pkrtz(y23[0], y23[1]));
-                return v4h{h01[0], h01[1], h23[0], h23[1]};
-            });
-            if (__builtin_amdgcn_ballot_w64(hi > kHi)) v_exact();
-        } else {
-            v_exact();
-        }
-        if (coh)
-            vt_tile_store<D, true>(T, lane, vd);
-        else
-            vt_tile_store<D, false>(T, lane, vd);
-    }
-    store_scales(sk, sv);
-    if (coh)
-        fused_flag(f.ctl, bh, g, G, lane);  // every store of the group has completed, then its flag
-    else if (lane == 0)
-        __hip_atomic_store(f.ctl.ready + (size_t)bh * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int D, int WAVES, int FL>
 __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 : 3)) void qmha_fa_int8_pipe_kernel(
     const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
     const float* __restrict__ sK, const float* __restrict__ sV,
     float* __restrict__ O, int N, int H, int d_model, int nqb, float c_log2, QkDump dbg,
-    const float* __restrict__ sQt = nullptr, int fair = 0, FusedKV fz = FusedKV{}) {
+    const float* __restrict__ sQt = nullptr, int fair = 0) {
     constexpr int SG = 2, RING = 3, PF = RING - 1;  // PF: stages in flight ahead
-    constexpr bool I8PV = FL & FL_I8PV;
-    constexpr int KBYTES = SG * 32 * D;                    // K int8 per stage
-    constexpr int VBYTES = SG * 32 * D * (I8PV ? 1 : 2);  // V int8 (FL_I8PV) or f16 per stage
+    constexpr int KBYTES = SG * 32 * D;      // K int8 per stage
+    constexpr int VBYTES = SG * 32 * D * 2;  // V f16 per stage
     constexpr int SBYTES = KBYTES + VBYTES;
     constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
     constexpr bool MAGIC = FL & FL_MAGIC;
@@ -587,21 +389,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // accumulates straight into O (the MFMA C operand); O is rescaled by alpha when a row's
     // running max moves (ballot-skipped otherwise) -- no P-tile max, no per-tile O fold
     constexpr bool PT = FL & FL_PT;
-    constexpr bool FUSED = FL & FL_FUSED;
-    static_assert(!(FUSED && (PT || DUMP)), "FL_FUSED: the per-block production kernel only");
-    // PT + FL_I8PV (A/B builds, -DQMHA_INT8_PT_I8PV=1): the per-tensor P@V on the i8 matrix core into an int32
-    // window that is folded into O when a row's running max moves (iter_pt)
-    constexpr bool PT8 = PT && I8PV;
-    static_assert(!PT8 || D == 32 || D == 64, "FL_PT | FL_I8PV: d = 32 / 64");
-    if constexpr (FUSED) {
-        // the K / V groups (qmha_fused.hpp); each wave's LDS transpose tile sits in the ring, which is not
-        // in use before the first DMA below (fused_produce_and_wait ends with a workgroup barrier)
-        char* T = reinterpret_cast<char*>(&lds[0][0]) + wave * (D * QMHA_VT_PITCH);
-        static_assert(WAVES * D * QMHA_VT_PITCH <= RING * SBYTES, "V^T tiles fit the ring");
-        fused_produce_and_wait<WAVES>(fz.ctl, wg, bh, nqb, G, wave, lane, [&](int pbh, int pg) {
-            produce_kv_group<D, I8PV>(fz, pbh, pg, H, N, G, d_model, lane, T);
-        });
-    }
     if (active) {
         const float* qrow = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D;
         const float sq = quant_q_operand<D>(qrow, half, qop, PT ? sQt[bh] : 0.0f);
@@ -617,16 +404,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         for (int ks = 0; ks < D / 32; ++ks) qop[ks] = v4i{0, 0, 0, 0};
     }
     const int8_t* kbase = Ki + (size_t)bh * N * D;
-    const char* vbase = reinterpret_cast<const char*>(Vh) + (size_t)bh * N * D * (I8PV ? 1 : 2);
-    const int sstride = PT ? 1 : (FUSED ? fz.sstride : G);  // PT: one scale per head slice
-    // FL_FUSED: these arrays are written by this launch, so their pointers pass through an opaque
-    // asm after the wait (no load through them can move above it), and the scales are then read
-    // through the constant address space (scalar loads, as the two-launch kernel's restrict pointers)
-    using SPtr = std::conditional_t<FUSED, const __attribute__((address_space(4))) float*, const float*>;
-    const float* skg = sK + (size_t)bh * sstride;
-    const float* svg = sV + (size_t)bh * sstride;
-    if constexpr (FUSED) asm volatile("" : "+s"(kbase), "+s"(vbase), "+s"(skg), "+s"(svg));
-    const SPtr skb = (SPtr)skg, svb = (SPtr)svg;
+    const char* vbase = reinterpret_cast<const char*>(Vh) + (size_t)bh * N * D * 2;
+    const int sstride = PT ? 1 : G;  // PT: one scale per head slice
+    const float* skb = sK + (size_t)bh * sstride;
+    const float* svb = sV + (size_t)bh * sstride;
     const int nst = (G + SG - 1) / SG;
 
     // K / V stages arrive by buffer_load ... lds: the per-lane source offsets are fixed, the
@@ -636,28 +417,18 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     constexpr bool SPREAD = WAVES >= KCH / 64 + VCH / 64;
     const int vw = SPREAD ? (wave + WAVES - KCH / 64) % WAVES : wave;
     int koff[KJ], voff[VJ];
-    // FL_FUSED: the offsets are computed from a copy of the lane id that an opaque asm makes available only
-    // here, so the compiler cannot hoist them above the K / V production, across which they would be spilled
-    // (and reloaded inside the sweep, each reload a vmcnt(0) wait that drains the LDS-DMA pipeline)
-    int lane_o = lane;
-    if constexpr (FUSED) asm volatile("" : "+v"(lane_o));
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
-        const int idx = (wave + jj * WAVES) * 64 + lane_o;
+        const int idx = (wave + jj * WAVES) * 64 + lane;
         const int row = idx / (D / 16), cc = swz_src<D>(row, idx % (D / 16));
         koff[jj] = row * D + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
-        const int idx = (vw + jj * WAVES) * 64 + lane_o;
-        if constexpr (I8PV) {  // 32-byte V^T rows (32 keys of one d), two 16-byte chunks each
-            const int r = idx >> 1, grp = r / D, d = r % D;
-            voff[jj] = grp * 32 * D + d * 32 + 16 * swz_src<32>(d, idx & 1);
-        } else {
-            const int grp = idx / (4 * D), w = idx % (4 * D);
-            const int d = w >> 2, cv = swz_src<64>(d, w & 3);
-            voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
-        }
+        const int idx = (vw + jj * WAVES) * 64 + lane;
+        const int grp = idx / (4 * D), w = idx % (4 * D);
+        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
+        voff[jj] = grp * 64 * D + d * 64 + 16 * cv;
     }
     // stage st into ring slot `slot` (= st % RING; a compile-time constant in the unrolled loop)
     auto issue_at = [&](int st, int slot) {
@@ -673,7 +444,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         for (int jj = 0; jj < VJ; ++jj) {
             const int inst = vw + jj * WAVES;
             if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
-                buffer_load_lds16(vbase, N * D * (I8PV ? 1 : 2), (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
+                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
         }
     };
     auto issue = [&](int st) { issue_at(st, st % RING); };
@@ -688,14 +459,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int d = 32 * m + col;
         return *reinterpret_cast<const v8h*>(L + KBYTES + par * 64 * D + d * 64 + 16 * swz_pos<64>(d, 2 * ks + half));
     };
-    auto vop8_at = [&](int slot, int par, int m) {  // FL_I8PV: the i8 V^T operand of d-block m (all 32 keys)
-        const int8_t* L = lds[slot];
-        const int d = 32 * m + col;
-        return *reinterpret_cast<const v4i*>(L + KBYTES + par * 32 * D + d * 32 + 16 * swz_pos<32>(d, half));
-    };
     auto kop_of = [&](int t, int ks) { return kop_at((t >> 1) % RING, t & 1, ks); };
     auto vop_of = [&](int t, int m, int ks) { return vop_at((t >> 1) % RING, t & 1, m, ks); };
-    auto vop8_of = [&](int t, int m) { return vop8_at((t >> 1) % RING, t & 1, m); };
 
     v16i magic_blk;
 #pragma unroll
@@ -708,7 +473,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // follow chunk c, in kOps order.  Every chained pair (same accumulator) is split by VALU.
     constexpr int MB = D / 32;  // 32-wide d-blocks of O^T (PV accumulators)
     constexpr int KS = D / 32;  // 32-deep k-steps of the i8 Q@K^T
-    constexpr int NOPS = (I8PV ? 1 : 2) * MB + KS;
+    constexpr int NOPS = 2 * MB + KS;
     constexpr int kSlot64[6] = {1, 1, 1, 1, 1, 1};
     constexpr int kOps64[6] = {0, 2, 1, 1000, 3, 1001};  // PV00 PV10 PV01 QK0 PV11 QK1
     constexpr int kSlot32[6] = {1, 0, 1, 1, 0, 0};
@@ -717,24 +482,10 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // d = 128: A PV00 PV10 | B PV20 QK0 | C PV30 PV01 | D QK1 PV11 | E PV21 QK2 | F PV31 QK3 -- every
     // chained pair (PV(m,0) -> PV(m,1), QK(k) -> QK(k+1)) is separated by a VALU chunk and another MFMA
     constexpr int kOps128[12] = {0, 2, 4, 1000, 6, 1, 1001, 3, 5, 1002, 7, 1003};
-    // FL_I8PV: one i8 P@V MFMA per d-block (op 2m), the Q@K^T chain split by VALU chunks as above
-    constexpr int kSlot64i[6] = {1, 1, 0, 1, 0, 1};
-    constexpr int kOps64i[4] = {0, 2, 1000, 1001};  // PV0 PV1 QK0 QK1
-    constexpr int kSlot32i[6] = {1, 0, 0, 1, 0, 0};
-    constexpr int kOps32i[2] = {0, 1000};  // PV0 QK0
-    constexpr int kSlot128i[6] = {2, 1, 2, 1, 1, 1};
-    constexpr int kOps128i[8] = {0, 2, 1000, 4, 1001, 6, 1002, 1003};  // A PV0 PV1 | B QK0 | C PV2 QK1 | D PV3 | E QK2 | F QK3
-    auto slot_n = [&](int c) {
-        if constexpr (I8PV) return D == 32 ? kSlot32i[c] : (D == 64 ? kSlot64i[c] : kSlot128i[c]);
-        else return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]);
-    };
-    auto op_at = [&](int i) {
-        if constexpr (I8PV) return D == 32 ? kOps32i[i] : (D == 64 ? kOps64i[i] : kOps128i[i]);
-        else return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]);
-    };
+    auto slot_n = [&](int c) { return D == 32 ? kSlot32[c] : (D == 64 ? kSlot64[c] : kSlot128[c]); };
+    auto op_at = [&](int i) { return D == 32 ? kOps32[i] : (D == 64 ? kOps64[i] : kOps128[i]); };
     static_assert(D == 32 || D == 64 || D == 128, "pipelined kernel: d in {32, 64, 128}");
-    static_assert(NOPS == (I8PV ? (D == 32 ? 2 : (D == 64 ? 4 : 8)) : (D == 32 ? 3 : (D == 64 ? 6 : 12))),
-                  "MFMA schedule table");
+    static_assert(NOPS == (D == 32 ? 3 : (D == 64 ? 6 : 12)), "MFMA schedule table");
 
     v16f o[MB];                  // O^T, d-block m (anchored)
 #pragma unroll
@@ -747,7 +498,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         s_nxt = __builtin_amdgcn_mfma_i32_32x32x32_i8(kk, qop[ks], ks == 0 ? magic_blk : s_nxt, 0, 0, 0);
     };
     v8h pc[2], pp[2];            // P^T operand halves (16 keys each) of tiles t (current) and t-1 (pending)
-    v4i pc8, pp8;                // FL_I8PV: the P^T operand as bytes (all 32 keys) of tiles t and t-1
     float scale_prev = 0.0f;
     v16f a[MB];                  // P@V accumulators of the pending tile
     constexpr bool JIT = FL & FL_JIT;  // operands read right before their MFMA (fewer live VGPRs)
@@ -791,7 +541,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float sp = fmaxf(pmax, 1.27e-6f) * (1.0f / 127.0f);
         h_invp = __builtin_amdgcn_rcpf(sp);
         h_invp *= h_f;
-        h_sp = I8PV ? sp : sp * 16777216.0f;  // FL_I8PV: P@V is the integer T itself
+        h_sp = sp * 16777216.0f;
     };
 
     issue(0);
@@ -815,7 +565,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int slot_nx = ph >= 0 ? (((2 + ph) >> 1) % RING) : (((t + 1) >> 1) % RING);
         const int par_n = ph >= 0 ? (ph & 1) : ((t + 1) & 1);
         auto vop = [&](int m, int ks) { return vop_at(slot_p, par_p, m, ks); };  // tile t-1
-        auto vop8 = [&](int m) { return vop8_at(slot_p, par_p, m); };            // tile t-1 (FL_I8PV)
         auto kop = [&](int ks) { return kop_at(slot_nx, par_n, ks); };           // tile t+1
         const int dma_st = (t >> 1) + PF;
         const int dma_slot = ph >= 0 ? ((((1 + ph) >> 1) + PF) % RING) : (((t >> 1) + PF) % RING);
@@ -832,18 +581,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         }
         // operand reads for this iteration's MFMAs (JIT: right before each MFMA instead)
         v8h vv[MB][2];
-        v4i vv8[MB];
         v4i kk[KS];
         if constexpr (has_prev && !JIT) {
-            if constexpr (I8PV) {
 #pragma unroll
-                for (int m = 0; m < MB; ++m) vv8[m] = vop8(m);
-            } else {
+            for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                    for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
-            }
+                for (int m = 0; m < MB; ++m) vv[m][ks] = vop(m, ks);
         }
         if constexpr (has_next && !JIT) {
 #pragma unroll
@@ -866,9 +609,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                             if constexpr (PT) {  // P@V straight into O
                                 o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks], o[m], 0,
                                                                               0, 0);
-                            } else if constexpr (I8PV) {  // T + 1.5 * 2^23 in every int32 lane (|T| < 2^22)
-                                a[m] = __builtin_bit_cast(v16f, __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                                    JIT ? vop8(m) : vv8[m], pp8, magic_blk, 0, 0, 0));
                             } else {
                                 a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
                                                                               ks == 0 ? v16f{} : a[m], 0, 0, 0);
@@ -928,24 +668,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // and those low 16 bits are exactly the f16 encoding of Pi * 2^-24; one byte permute
         // packs two entries.  P@V then yields T * 2^-24 exactly (T < 2^20); the O scale
         // carries the 2^24 back.
-        if constexpr (I8PV) {  // FL_I8PV: byte e of dword k = Pi of S register 4k + e (the i8 B operand's slot order)
 #pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) {
-                uint32_t tq[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) tq[e] = __float_as_uint(fmaf(p[4 * k4 + e], invp, QMHA_MAGIC_RNE));
-                const uint32_t t01 = __builtin_amdgcn_perm(tq[1], tq[0], 0x0c0c0400u);
-                const uint32_t t23 = __builtin_amdgcn_perm(tq[3], tq[2], 0x0c0c0400u);
-                pc8[k4] = (int)__builtin_amdgcn_perm(t23, t01, 0x05040100u);
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
-                const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
-                pc[r >> 2][2 * (r & 3)] = h2[0];
-                pc[r >> 2][2 * (r & 3) + 1] = h2[1];
-            }
+        for (int r = 0; r < 8; ++r) {
+            const float t0 = fmaf(p[2 * r], invp, QMHA_MAGIC_RNE), t1 = fmaf(p[2 * r + 1], invp, QMHA_MAGIC_RNE);
+            const v2h h2 = __builtin_bit_cast(v2h, __builtin_amdgcn_perm(__float_as_uint(t1), __float_as_uint(t0), 0x05040100u));
+            pc[r >> 2][2 * (r & 3)] = h2[0];
+            pc[r >> 2][2 * (r & 3) + 1] = h2[1];
         }
         QMHA_FENCE();
         mfmas(5);
@@ -958,8 +686,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         else
             l_run = fmaf(rs, e * h_f, l_run);
         m_run = m_new;
-        // sp carries 2^24 (P entries are Pi * 2^-24) except under FL_I8PV (P@V is T itself): the same products,
-        // scaled by 2^24 exactly, so both forms fold the same rounded values
+        // sp carries 2^24 (P entries are Pi * 2^-24)
         const float scale_t = PT ? 0.0f : sp * svb[t] * e;
         // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor)); PT: O already
         // holds tile t-1's P@V, and takes this tile's alpha before tile t's P@V lands next iteration
@@ -971,34 +698,13 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         } else if constexpr (has_prev) {
 #pragma unroll
             for (int m = 0; m < MB; ++m)
-                if constexpr (I8PV) {  // o += T * s with T = A - 1.5 * 2^23 (exact), packed
 #pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        const v2f tt = v2f{a[m][r], a[m][r + 1]} - v2f{QMHA_MAGIC_RNE, QMHA_MAGIC_RNE};
-                        const v2f u = __builtin_elementwise_fma(tt, v2f{scale_prev, scale_prev}, v2f{o[m][r], o[m][r + 1]});
-                        o[m][r] = u[0];
-                        o[m][r + 1] = u[1];
-                    }
-                } else {
-#if QMHA_FOLD_PK  // A/B: the fold as packed fp32 fmas (16 v_pk_fma instead of 32 v_fmac per d-block)
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        const v2f u = __builtin_elementwise_fma(v2f{a[m][r], a[m][r + 1]}, v2f{scale_prev, scale_prev},
-                                                                v2f{o[m][r], o[m][r + 1]});
-                        o[m][r] = u[0];
-                        o[m][r + 1] = u[1];
-                    }
-#else
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
-#endif
-                }
+                for (int r = 0; r < 16; ++r) o[m][r] = fmaf(a[m][r], scale_prev, o[m][r]);
         }
         QMHA_FENCE();
         // rotate the pipeline
         pp[0] = pc[0];
         pp[1] = pc[1];
-        if constexpr (I8PV) pp8 = pc8;
         scale_prev = scale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
@@ -1010,39 +716,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
     // P@V of t-2 has), so no MFMA result is waited on.
     float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
-    // PT8: P@V of the tiles since the last fold accumulates exactly in the int32 window w8 (every tile of a
-    // window quantised against the same running max m_w).  When some row's max moves, the window is folded
-    // into O in anchor units, o += W * 2^(m_w - anchor) (one conversion and one fma per element, no O
-    // rescale: the anchored O of the per-block kernel), and restarted.  |W| < 2^31 for up to 4160 tiles
-    // of 32 keys (32 * 127 * 127 each): int8_pt_v8 limits N to 131072.
-    v16i w8[MB];
-#pragma unroll
-    for (int m = 0; m < MB; ++m) w8[m] = v16i{};
-    float m_w = 0.0f, f_w = 1.0f;
-    auto fold8 = [&]() {
-#pragma unroll
-        for (int m = 0; m < MB; ++m) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[m][r] = fmaf((float)w8[m][r], f_w, o[m][r]);
-            // restart the window: 8 64-bit moves per d-block (the compiler's zeroing is 16 32-bit ones)
-            v2i z[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) asm volatile("v_mov_b64 %0, 0" : "=v"(z[i]));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                w8[m][2 * i] = z[i][0];
-                w8[m][2 * i + 1] = z[i][1];
-            }
-        }
-        m_w = m_run;
-        if (__builtin_amdgcn_ballot_w64(m_w - anchor > 48.0f)) {  // keep 2^(m - anchor) <= 2^48 (rare)
-            const float g = __builtin_amdgcn_exp2f(anchor - m_w);
-#pragma unroll
-            for (int m = 0; m < MB; ++m) o[m] *= g;
-            anchor = m_w;
-        }
-        f_w = __builtin_amdgcn_exp2f(m_w - anchor);
-    };
     auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
         constexpr int ph = decltype(PH)::value;
@@ -1065,20 +738,14 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
             }
         }
         v8h vv[MB][2];
-        v4i vv8[MB];
         v4i kk[KS];
-        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs (PT8: the k-step-0 P@V slots, one i8 MFMA per d-block)
+        auto rd_slot = [&](int s) {  // operands of slot s's MFMAs
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int op = pt_slot_op(D, s, j);
                 if (op >= 0 && op < 8) {
-                    if constexpr (has_prev) {
-                        if constexpr (PT8) {
-                            if ((op & 1) == 0 && (op >> 1) < MB) vv8[(op >> 1) % MB] = vop8_at(slot_p, par_p, op >> 1);
-                        } else if ((op >> 1) < MB) {
-                            vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
-                        }
-                    }
+                    if constexpr (has_prev)
+                        if ((op >> 1) < MB) vv[(op >> 1) % MB][op & 1] = vop_at(slot_p, par_p, op >> 1, op & 1);
                 } else if (op >= 8) {
                     if constexpr (has_next)
                         if (op - 8 < KS) kk[(op - 8) % KS] = kop_at(slot_nx, par_n, op - 8);
@@ -1092,12 +759,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 if (op >= 0 && op < 8) {
                     if constexpr (has_prev) {
                         const int m = (op >> 1) % MB;
-                        if constexpr (PT8) {
-                            if ((op & 1) == 0 && (op >> 1) < MB)
-                                w8[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vv8[m], pp8, w8[m], 0, 0, 0);
-                        } else if ((op >> 1) < MB) {
-                            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][op & 1], pp[op & 1], o[m], 0, 0, 0);
-                        }
+                        if ((op >> 1) < MB) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[m][op & 1], pp[op & 1], o[m], 0, 0, 0);
                     }
                 } else if (op >= 8) {
                     if constexpr (has_next)
@@ -1117,17 +779,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 if (r >= r0 && r < r1) q[r] = fmaf(p[r], h_invp, QMHA_MAGIC_RNE);
         };
         auto perms = [&](int j0, int j1) {
-            if constexpr (PT8) {  // bytes: byte e of dword k = Pi of S register 4k + e (the i8 B operand's slot order)
-#pragma unroll
-                for (int k4 = 0; k4 < 4; ++k4)
-                    if (2 * k4 >= j0 && 2 * k4 < j1) {
-                        const uint32_t t01 = __builtin_amdgcn_perm(__float_as_uint(q[4 * k4 + 1]), __float_as_uint(q[4 * k4]), 0x0c0c0400u);
-                        const uint32_t t23 = __builtin_amdgcn_perm(__float_as_uint(q[4 * k4 + 3]), __float_as_uint(q[4 * k4 + 2]), 0x0c0c0400u);
-                        pc8[k4] = (int)__builtin_amdgcn_perm(t23, t01, 0x05040100u);
-                    }
-                asm volatile("" : "+v"(pc8));
-                return;
-            }
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (j >= j0 && j < j1) {
@@ -1146,9 +797,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float c = h_c, kn = h_k;
         QMHA_FENCE();
         if constexpr (has_prev) {
-            if constexpr (PT8) {  // the window's tiles (<= t-2) and tile t-1 were quantised against different maxima
-                if (__builtin_amdgcn_ballot_w64(m_run != m_w)) fold8();
-            } else if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
             }
@@ -1213,12 +862,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         QMHA_FENCE();
         mf_slot(5);
         QMHA_FENCE();
-        if constexpr (PT8) {
-            pp8 = pc8;
-        } else {
-            pp[0] = pc[0];
-            pp[1] = pc[1];
-        }
+        pp[0] = pc[0];
+        pp[1] = pc[1];
         alpha_prev = h_alpha;
         if constexpr (has_next) s_cur = s_nxt;
     };
@@ -1272,15 +917,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // drain: P@V of the last tile
     {
         const int t = G - 1;
-        if constexpr (PT8) {
-            if (__builtin_amdgcn_ballot_w64(m_run != m_w)) fold8();
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                w8[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(vop8_of(t, m), pp8, w8[m], 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] = fmaf((float)w8[m][r], f_w, o[m][r]);
-            }
-        } else if constexpr (PT) {
+        if constexpr (PT) {
             if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {  // O still owes the last tile's alpha
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
@@ -1290,13 +927,6 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
 #pragma unroll
                 for (int m = 0; m < MB; ++m)
                     o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vop_of(t, m, ks), pp[ks], o[m], 0, 0, 0);
-        } else if constexpr (I8PV) {
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                const v16i ai = __builtin_amdgcn_mfma_i32_32x32x32_i8(vop8_of(t, m), pp8, magic_blk, 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[m][r] += (__int_as_float(ai[r]) - QMHA_MAGIC_RNE) * scale_prev;
-            }
         } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -1312,10 +942,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     if (active) {
         // PT: O is in units of 2^-24 (the f16-subnormal P entries) times sV / 127: 2^24 * sV / 127
         // rescales it exactly to the oracle's O * (sV / 127)
-        // PT8: O is in units of sV / 127 times 2^(m - anchor)
-        const float unanchor = PT8  ? __builtin_amdgcn_exp2f(anchor - m_run) * (svb[0] / 127.0f)
-                               : PT ? 16777216.0f * (svb[0] / 127.0f)
-                                    : __builtin_amdgcn_exp2f(anchor - m_run);
+        const float unanchor = PT ? 16777216.0f * (svb[0] / 127.0f) : __builtin_amdgcn_exp2f(anchor - m_run);
         const float l = PT ? half_swap_add(l_run) : half_swap_add(l_run) * unanchor;
         const bool ok = l > 1e-20f;
         float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + col) * d_model + (size_t)k * D + 4 * half;
@@ -1355,32 +982,26 @@ __global__ __launch_bounds__(64) void qmha_debug_qk_int32_kernel(const int8_t* _
 // ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
-// Production layout: Ki, Vh, sK, sV (the main kernel quantises Q in registers).  with_q adds Qi
-// and sQ at the end for the int32 Q@K^T test hook, whose pre-pass quantises Q too.
-// The scale arrays hold [B*H][int8_scale_stride(N)] floats: the fused kernel pads each head's
-// scales to whole 128-byte lines (the two-launch path uses the first B*H*G of them, [B*H][G]).
-// kv_ready: the fused kernel's group flags [B*H][G].
-int int8_scale_stride(int N) { return (int)align_up((size_t)(N / QMHA_GROUP), 32); }
+// Production layout: Ki [B*H][N][D], Vh (f16 V^T operand blocks, 2 bytes per element), sK, sV
+// [B*H][N/32] (the main kernel quantises Q in registers).  with_q adds Qi and sQ at the end for the
+// int32 Q@K^T test hook, whose pre-pass quantises Q too.
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q) {
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t s = align_up((size_t)B * H * int8_scale_stride(N) * sizeof(float), 256);
-    const size_t f = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(uint32_t), 256);
-    return e + 2 * e + 2 * s + f + (with_q ? e + s : 0);
+    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
+    return e + 2 * e + 2 * s + (with_q ? e + s : 0);
 }
 
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q) {
     Int8Workspace w{};
     const size_t e = align_up((size_t)B * H * N * D, 256);
-    const size_t s = align_up((size_t)B * H * int8_scale_stride(N) * sizeof(float), 256);
-    const size_t f = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(uint32_t), 256);
+    const size_t s = align_up((size_t)B * H * (N / QMHA_GROUP) * sizeof(float), 256);
     char* p = static_cast<char*>(ws);
     w.Ki = reinterpret_cast<int8_t*>(p);
     w.Vh = reinterpret_cast<_Float16*>(p + e);
     w.sK = reinterpret_cast<float*>(p + 3 * e);
     w.sV = reinterpret_cast<float*>(p + 3 * e + s);
-    w.kv_ready = reinterpret_cast<uint32_t*>(p + 3 * e + 2 * s);
-    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s + f) : nullptr;
-    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s + f) : nullptr;
+    w.Qi = with_q ? reinterpret_cast<int8_t*>(p + 3 * e + 2 * s) : nullptr;
+    w.sQ = with_q ? reinterpret_cast<float*>(p + 4 * e + 2 * s) : nullptr;
     return w;
 }
 
@@ -1433,51 +1054,7 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     const int rounds = pipe_rounds<D, WAVES, FL>((long long)B * H * nqb);
     const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
-                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)nullptr, fair, FusedKV{});
-    return hipGetLastError();
-}
-
-// ---- FL_FUSED launch: zero the group flags, then the pipelined kernel that quantises K / V itself
-__global__ __launch_bounds__(256) void qmha_zero_flags_kernel(uint32_t* __restrict__ p, int n) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) p[i] = 0u;
-}
-// 0 two launches (the default: the fused kernel is an opt-in until it has GPU evidence), 1 fused,
-// 2 fused with the cross-XCD test rule
-static std::atomic<int> g_fused_mode{0};
-static std::atomic<long long> g_fused_wait{5000};     // 50 us
-static std::atomic<int> g_fused_ablate{0};            // FusedCtl::ablate (measurements only)
-int set_int8_fused(int mode) { return g_fused_mode.exchange(mode); }
-int set_int8_fused_ablate(int bits) { return g_fused_ablate.exchange(bits); }
-long long set_int8_fused_wait(long long ticks) { return g_fused_wait.exchange(ticks); }
-bool int8_fused_on(int D, int N) { return g_fused_mode.load() != 0 && (D == 32 || D == 64 || D == 128) && N / QMHA_GROUP >= 2; }
-
-template <int D, int WAVES, int FL>
-static hipError_t fa_int8_fused_launch(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O,
-                                       int B, int N, int H, int d_model, hipStream_t stream) {
-    constexpr int FLF = FL | FL_FUSED;
-    const int G = N / QMHA_GROUP;
-    const int nqb = (G + WAVES - 1) / WAVES;
-    const long long nwg = (long long)B * H * nqb;
-    const long long slots = pipe_slots<D, WAVES, FLF>();
-    if (nwg > INT32_MAX) return hipErrorInvalidValue;
-    const int R = (int)(slots / 8 > 0 ? slots / 8 : 1);
-    if (slots <= 0 || nqb > R) {  // occupancy unknown, or a head longer than a round of an XCD: the split's
-                                  // producers would run after their consumers (tests/test_fused_schedule.py);
-                                  // the two launches instead
-        hipError_t e = launch_quant_int8(Qf, Kf, Vf, w, w.Vh, (FL & FL_I8PV) ? 0 : 1, B, N, H, D, d_model, stream,
-                                         /*first_tensor=*/1);
-        return e != hipSuccess ? e : fa_int8_pipe_launch<D, WAVES, FL>(w, Qf, O, B, N, H, d_model, stream);
-    }
-    const int nflags = B * H * G;
-    hipLaunchKernelGGL(qmha_zero_flags_kernel, dim3((nflags + 255) / 256), dim3(256), 0, stream, w.kv_ready, nflags);
-    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
-    const int rounds = (int)((nwg + slots - 1) / slots);
-    const int fair = rounds <= kFairMaxRounds;
-    FusedKV fz{Kf, Vf, w.Ki, w.Vh, w.sK, w.sV, int8_scale_stride(N),
-               FusedCtl{w.kv_ready, R, g_fused_mode.load() == 2 ? 1 : 0, g_fused_wait.load(), g_fused_ablate.load()}};
-    hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FLF>), dim3((int)nwg), dim3(WAVES * 64), 0, stream, Qf, w.Ki,
-                       w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, QkDump{}, (const float*)nullptr, fair, fz);
+                       w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)nullptr, fair);
     return hipGetLastError();
 }
 
@@ -1513,7 +1090,7 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
     const int rounds = pipe_rounds<D, WAVES, FL | FL_PT>((long long)B * H * nqb);
     const int fair = rounds > 0 && rounds <= kFairMaxRounds;
     hipLaunchKernelGGL((qmha_fa_int8_pipe_kernel<D, WAVES, FL | FL_PT>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream,
-                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ, fair, FusedKV{});
+                       Qf, w.Ki, w.Vh, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg, (const float*)w.sQ, fair);
     return hipGetLastError();
 }
 
@@ -1523,49 +1100,21 @@ static hipError_t fa_int8_pt_launch(const Int8Workspace& w, const float* Qf, flo
 // with the magic-biased accumulator at a 2-wave budget, 1 wave above d = 128 (O alone is d/2 VGPRs
 // per lane; at 2 waves d = 160 / 192 spill 176 / 372 bytes per lane to scratch).
 constexpr int kD64Flags = FL_MAGIC | FL_KFOLD, kD32Flags = FL_MAGIC | FL_KFOLD;
-#ifndef QMHA_INT8_W64
-#define QMHA_INT8_W64 4  // waves per workgroup of the per-block d = 64 kernel (A/B builds: -DQMHA_INT8_W64=12)
-#endif
 constexpr int kD128Flags = FL_MAGIC | FL_KFOLD | FL_JIT | FL_LB2, kPtD32Extra = FL_LB4;
-// the per-block pipelined kernels' P@V on the i8 matrix core (FL_I8PV; A/B builds: -DQMHA_INT8_I8PV=0|1)
-#ifndef QMHA_INT8_I8PV
-#define QMHA_INT8_I8PV 0
-#endif
-// (d = 32 / 64; the d = 128 schedule, operands read at their MFMA under a 2-wave budget, spills with it)
-template <int D>
-constexpr int kPbExtra = (QMHA_INT8_I8PV && (D == 32 || D == 64)) ? FL_I8PV : 0;
-// V layout the per-block pre-pass writes for this call: 0 = int8 in the i8 V^T operand order (the pipelined
-// kernels under FL_I8PV), 1 = f16 integers (the f16 P@V form, and the one-tile kernel: N = 32, other d)
-int int8_v_mode(int D, int N) {
-    const bool i8pv = D == 32 ? kPbExtra<32> != 0 : (D == 64 ? kPbExtra<64> != 0 : false);
-    return (i8pv && N / QMHA_GROUP >= 2) ? 0 : 1;
-}
 template <int D>
 constexpr int kAnyFlags = FL_MAGIC | (D > 128 ? FL_LB1 : FL_LB2);
 
 template <int D, int XFL = 0>
 static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                             hipStream_t stream, QkDump dbg = QkDump{}) {
-    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | kPbExtra<32> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    else if constexpr (D == 64)
-        return fa_int8_pipe_launch<D, QMHA_INT8_W64, kD64Flags | kPbExtra<64> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-    else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | kPbExtra<128> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    if constexpr (D == 32) return fa_int8_pipe_launch<D, 4, kD32Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 64) return fa_int8_pipe_launch<D, 4, kD64Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
+    else if constexpr (D == 128) return fa_int8_pipe_launch<D, 4, kD128Flags | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
-}
-
-// the per-tensor kernels' P@V on the i8 matrix core into an int32 window (PT + FL_I8PV; A/B builds:
-// -DQMHA_INT8_PT_I8PV=0|1, qmha_kernels.hpp; d = 32 / 64, at least two tiles, N <= 131072 for the window's int32 range)
-bool int8_pt_v8(int D, int N) {
-    return QMHA_INT8_PT_I8PV && (D == 32 || D == 64) && N / QMHA_GROUP >= 2 && N <= 131072;
 }
 
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, hipStream_t stream) {
-#if QMHA_INT8_PT_I8PV
-    if (int8_pt_v8(D, N))
-        return D == 32 ? fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_I8PV>(w, Qf, O, B, N, H, d_model, stream)
-                       : fa_int8_pt_launch<64, kD64Flags | FL_I8PV>(w, Qf, O, B, N, H, d_model, stream);
-#endif
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra>(w, Qf, O, B, N, H, d_model, stream);
         case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
@@ -1575,17 +1124,6 @@ hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float
 }
 
 #define QMHA_INT8_D_CASES(X) X(32) X(64) X(96) X(128) X(160) X(192) X(224) X(256)
-
-hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
-                                int N, int H, int D, int d_model, hipStream_t stream) {
-    if (!int8_fused_on(D, N) || !w.kv_ready) return hipErrorInvalidValue;
-    switch (D) {
-        case 32: return fa_int8_fused_launch<32, 4, kD32Flags | kPbExtra<32>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 64: return fa_int8_fused_launch<64, 4, kD64Flags | kPbExtra<64>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        case 128: return fa_int8_fused_launch<128, 4, kD128Flags | kPbExtra<128>>(w, Qf, Kf, Vf, O, B, N, H, d_model, stream);
-        default: return hipErrorInvalidValue;
-    }
-}
 
 hipError_t launch_fa_int8_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                int d_model, hipStream_t stream) {
@@ -1616,11 +1154,6 @@ hipError_t launch_fa_int8_dump(const Int8Workspace& w, const float* Qf, float* O
 // launch_fa_int8_pt_main, plus the stores)
 hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, QkDump dbg, hipStream_t stream) {
-#if QMHA_INT8_PT_I8PV  // the production instance's twin (the pre-pass wrote V for it)
-    if (int8_pt_v8(D, N))
-        return D == 32 ? fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_I8PV | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg)
-                       : fa_int8_pt_launch<64, kD64Flags | FL_I8PV | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
-#endif
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 64: return fa_int8_pt_launch<64, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);

@@ -23,23 +23,9 @@ struct Int8Workspace {
     float* sK;
     float* sV;
     uint32_t* slice_sync;  // per-tensor mode only: [2][3][B*H] slice absmax bits and part arrivals (qmha_pt_quant_kernel)
-    uint32_t* kv_ready;    // per-block fused kernel only: [B*H][N/32] group flags
 };
 size_t int8_workspace_bytes(int B, int N, int H, int D, bool with_q = false);
 Int8Workspace int8_carve(void* ws, int B, int N, int H, int D, bool with_q = false);
-int int8_scale_stride(int N);  // scales per head in the int8 workspace (N/32 rounded up to 32)
-int int8_v_mode(int D, int N);  // the per-block pre-pass's V layout for this call (launch_quant_int8 v_mode)
-// The fused per-block call (FL_FUSED): K / V quantised by the main kernel's own workgroups, one
-// launch plus a flag-zeroing one.  int8_fused_on: whether run() takes it (d = 32 / 64 / 128, N >= 64,
-// switched on); set_int8_fused: 0 off (pre-pass + main, the default), 1 on, 2 on with the test rule that
-// has every group produced on another XCD; set_int8_fused_wait: the wait bound in 100 MHz ticks
-// (0 forces every wave to produce its share of its head itself).  Both return the previous value.
-bool int8_fused_on(int D, int N);
-int set_int8_fused(int mode);
-long long set_int8_fused_wait(long long ticks);
-int set_int8_fused_ablate(int bits);  // FusedCtl::ablate, measurements only
-hipError_t launch_fa_int8_fused(const Int8Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
-                                int N, int H, int D, int d_model, hipStream_t stream);
 // v_mode 0: V to `vout` as int8 in the i8 operand order; 1: as f16 integers (main path)
 // first_tensor = 1 skips Q (the main kernels quantise Q themselves); 0 quantises Q, K, V;
 // num_tensors (default: all from first_tensor on) limits the roles launched (the standalone op)
@@ -50,12 +36,6 @@ hipError_t launch_quant_int8(const float* Q, const float* K, const float* V, con
 // layout: Ki, Vh as fa_tc_int8_b, then slice_sync [2][3][B*H] uint32, then sQ, sK, sV [B*H] each
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D);
 Int8Workspace int8_pt_carve(void* ws, int B, int N, int H, int D);
-// whether this call's per-tensor main kernel runs P@V on the i8 matrix core (FL_I8PV, A/B builds
-// -DQMHA_INT8_PT_I8PV=1; d = 32 / 64): then the pre-pass writes V as int8 in the i8 V^T operand order
-#ifndef QMHA_INT8_PT_I8PV
-#define QMHA_INT8_PT_I8PV 0
-#endif
-bool int8_pt_v8(int D, int N);
 // one pass: K / V quantised with their head-slice scales from registers, sQ (qmha_pt_quant_kernel)
 // the per-tensor pre-pass's bounded wait in 100 MHz ticks (default 200000 = 2 ms; 0 forces the
 // fallback); returns the previous value
@@ -88,19 +68,9 @@ struct F16Workspace {
     _Float16* Qh;  // unused (nullptr): the main kernel converts Q in registers
     _Float16* Kh;  // [B*H][N][D]
     _Float16* Vt;  // [B*H][N/32][D][32]  (f16 operand slot order)
-    uint32_t* kv_ready;  // fused kernel only: [B*H][N/32] group flags
 };
 size_t f16_workspace_bytes(int B, int N, int H, int D);
 F16Workspace f16_carve(void* ws, int B, int N, int H, int D);
-// The fused fp16 call (F16_FUSED): K / V converted by the main kernel's own workgroups with
-// the int8 fused kernel's split and flags (qmha_fused.hpp).  f16_fused_on: whether run() takes it
-// (d = 32 / 64 / 128, switched on); set_f16_fused: 0 off (pre-pass + main), 1 on, 2 on with the cross-XCD
-// test rule.  Returns the previous mode.
-bool f16_fused_on(int D, int N);
-int set_f16_fused(int mode);
-hipError_t launch_fa_f16_fused(const F16Workspace& w, const float* Qf, const float* Kf, const float* Vf, float* O, int B,
-                               int N, int H, int D, int d_model, hipStream_t stream);
-hipError_t launch_zero_u32(uint32_t* p, int n, hipStream_t stream);
 hipError_t launch_convert_f16(const float* Q, const float* K, const float* V, const F16Workspace& w, int B, int N,
                               int H, int D, int d_model, hipStream_t stream);
 hipError_t launch_fa_f16_main(const F16Workspace& w, const float* Qf, float* O, int B, int N, int H, int D, int d_model,

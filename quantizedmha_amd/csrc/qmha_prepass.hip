@@ -294,15 +294,11 @@ static hipError_t quant_int8_d(const float* Q, const float* K, const float* V, c
 // workgroup reduces the whole slice itself (the same maximum), so no dispatch order can deadlock it.
 // sync = [2][3][B*H] uint32 (max bits, arrivals), zeroed by qmha_zero_u32_kernel in the same call.
 // ---------------------------------------------------------------------------------------
+// (zeroed by a kernel, not hipMemsetAsync: under graph capture a memset node did not re-zero on replays,
+// DESIGN.md 5.2b)
 __global__ __launch_bounds__(256) void qmha_zero_u32_kernel(uint32_t* __restrict__ p, int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[i] = 0u;
-}
-// a kernel, not hipMemsetAsync: under graph capture a memset node did not re-zero on replays
-hipError_t launch_zero_u32(uint32_t* p, int n, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(qmha_zero_u32_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, n);
-    return hipGetLastError();
 }
 
 // The part's absmax into the slice maximum, PERFORMED before the caller's arrival increment: a
@@ -329,8 +325,7 @@ __device__ __forceinline__ float wg_max(const float (&pm)[kPtWaves]) {
 template <int D>
 constexpr int pt_groups_per_wave() { return D == 128 ? 1 : 256 / D; }
 
-// V8: V as int8 in the i8 V^T operand order (the per-tensor main kernel under FL_I8PV, int8_pt_v8); else f16 integers
-template <int D, bool V8 = false>
+template <int D>
 __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int8_t* __restrict__ Ki,
     _Float16* __restrict__ Vh, float* __restrict__ sQ, float* __restrict__ sK, float* __restrict__ sV,
@@ -464,9 +459,7 @@ __global__ __launch_bounds__(64 * kPtWaves) void qmha_pt_quant_kernel(
         const int g = part * GPB + wave * PW + j;
         if (g >= G) continue;  // wave-uniform
         if (isv) {
-            if constexpr (V8)
-                vt8_group_store<D>(vtr[wave], x[j], inv, lane, reinterpret_cast<char*>(Vh) + ((size_t)bh * G + g) * (size_t)(32 * D));
-            else if (Vh)
+            if (Vh)
                 vt_group_store<D, true>(vtr[wave], x[j], inv, lane,
                                         reinterpret_cast<char*>(Vh) + ((size_t)bh * G + g) * (size_t)(64 * D));
         } else {
@@ -493,7 +486,7 @@ long long set_pt_wait_ticks(long long ticks) { return g_pt_wait_ticks.exchange(t
 
 // workgroups of qmha_pt_quant_kernel<D> one XCD holds at once (HIP's occupancy answer x CUs / 8 XCDs,
 // cached per device); 0 if unknown
-template <int D, bool V8>
+template <int D>
 static int pt_resident_per_xcd() {
     static std::atomic<int> cache[64];
     int dev = 0;
@@ -501,7 +494,7 @@ static int pt_resident_per_xcd() {
     int r = cache[dev].load(std::memory_order_relaxed);
     if (r <= 0) {
         int n = 0, c = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, qmha_pt_quant_kernel<D, V8>, 64 * kPtWaves, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, qmha_pt_quant_kernel<D>, 64 * kPtWaves, 0) != hipSuccess ||
             hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0 || c <= 0)
             return 0;
         r = n * c / 8;
@@ -512,7 +505,7 @@ static int pt_resident_per_xcd() {
 
 // single-read launch (qmha_pt_quant_kernel): per head slice its K parts, V parts, Q parts (12 waves x
 // pt_groups_per_wave<D>() groups each); the slice counters / maxima zeroed by a kernel of this call
-template <int D, bool V8 = false>
+template <int D>
 static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                    int H, int d_model, bool rows_only, hipStream_t stream) {
     const int G = N / QMHA_GROUP, BH = B * H;
@@ -527,16 +520,16 @@ static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* 
     // holds (d = 128 beyond N = 12288, d = 64 beyond 49152, d = 32 beyond 98304 at one workgroup per CU)
     // would leave each part waiting out the bound -- those run the two-pass form instead: phase 1 publishes
     // every part's absmax, phase 2 re-reads K / V and quantises them with the slice maxima (round-4 ADVICE)
-    const int resident = pt_resident_per_xcd<D, V8>();
+    const int resident = pt_resident_per_xcd<D>();
     const long long wait_ticks = g_pt_wait_ticks.load();
     if (resident <= 0 || gkv > resident || wait_ticks < 0) {
         for (int phase = 1; phase <= 2; ++phase)
-            hipLaunchKernelGGL((qmha_pt_quant_kernel<D, V8>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
+            hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
                                rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1,
                                kv_tensors, with_q, 0ull, phase);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((qmha_pt_quant_kernel<D, V8>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
+    hipLaunchKernelGGL((qmha_pt_quant_kernel<D>), dim3(grid), dim3(64 * kPtWaves), 0, stream, Q, K, V, w.Ki,
                        rows_only ? nullptr : w.Vh, w.sQ, w.sK, w.sV, sync, N, H, d_model, BH, gkv, gkv, 1, kv_tensors,
                        with_q, (unsigned long long)wait_ticks, 0);
     return hipGetLastError();
@@ -545,9 +538,6 @@ static hipError_t quant_int8_pt1_d(const float* Q, const float* K, const float* 
 template <int D>
 static hipError_t quant_int8_pt_d(const float* Q, const float* K, const float* V, const Int8Workspace& w, int B, int N,
                                   int H, int d_model, hipStream_t stream) {
-    if constexpr (QMHA_INT8_PT_I8PV && (D == 32 || D == 64)) {
-        if (int8_pt_v8(D, N)) return quant_int8_pt1_d<D, true>(Q, K, V, w, B, N, H, d_model, false, stream);
-    }
     return quant_int8_pt1_d<D>(Q, K, V, w, B, N, H, d_model, false, stream);
 }
 

@@ -163,7 +163,7 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     syms = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
     stubs = set(re.findall(r"__device_stub__(\w+?)ILi(\d+)E(\w*)", syms))
     per = {}
-    dumps, fused, fused16 = [], [], []
+    dumps = []
     for name, d, rest in stubs:
         if name.startswith("qmha_gemm"):
             continue
@@ -171,13 +171,6 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
             m, fl = re.match(r"Li(\d+)ELi(\d+)E", rest), 2
         elif name == "qmha_fa_int8_kernel":  # <D, FL> (the one-tile kernel: N = 32, and d outside 32/64/128)
             m, fl = re.match(r"Li(\d+)E", rest), 1
-        elif name == "qmha_fa_f16_v2_kernel":  # <D, WAVES, SG, FL>: F16_FUSED (64) twins of the production instance
-            mf = re.match(r"Li(\d+)ELi(\d+)ELi(\d+)E", rest)
-            if mf and int(mf.group(3)) & 64:
-                f = mf.group(3)
-                fused16.append((name, d, rest.replace(f"ELi{f}E", f"ELi{int(f) & ~64}E", 1)))
-                continue
-            m = None
         else:
             m = None
         if m and int(m.group(fl)) & 1048576:  # FL_PT: the fa_tc_int8_pt variant's own instance
@@ -188,19 +181,7 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
                 rest.replace(f"ELi{f}E", f"ELi{int(f) & ~256}E", 1)
             dumps.append((name, d, twin))
             continue
-        if m and fl == 2 and int(m.group(fl)) & 2097152:  # FL_FUSED: the same schedule plus the K / V production
-            f = m.group(fl)
-            fused.append((name, d, rest.replace(f"ELi{f}E", f"ELi{int(f) & ~2097152}E", 1)))
-            continue
         per.setdefault((name, d), set()).add(rest)
-    # the fused per-block kernel at d = 32 / 64 / 128 is the two-launch schedule with FL_FUSED added
-    assert sorted(d for _, d, _ in fused) == ["128", "32", "64"], fused
-    for name, d, base in fused:
-        assert per[(name, d)] == {base}, (name, d, base)
-    # likewise the fused fp16 kernel (F16_FUSED) at d = 32 / 64 / 128
-    assert sorted(d for _, d, _ in fused16) == ["128", "32", "64"], fused16
-    for name, d, base in fused16:
-        assert per[(name, d)] == {base}, (name, d, base)
     # per-block d = 32 / 64 / 128 (pipelined) and 96 / 160 / 192 / 224 / 256 (one-tile kernel),
     # per-tensor d = 32 / 64 / 128
     assert len(dumps) == 11, dumps

@@ -54,21 +54,3 @@ def test_ablation_sources_compile(tmp_path):
     with cf.ThreadPoolExecutor(len(srcs)) as ex:
         for n, r in ex.map(compile_one, srcs):
             assert r.returncode == 0, n + ": " + r.stderr[-3000:]
-
-
-def test_ab_build_options_compile(tmp_path):
-    """The A/B build options of the int8 kernels compile together (QMHA_INT8_I8PV, the per-block
-    P@V on the i8 matrix core; QMHA_INT8_PT_I8PV, the per-tensor one into an int32 window, with the pre-pass's
-    int8 V; QMHA_FOLD_PK, the packed fold), compile-only."""
-    import concurrent.futures as cf
-    csrc = os.path.join(ROOT, "quantizedmha_amd", "csrc")
-    flags = ["-DQMHA_INT8_I8PV=1", "-DQMHA_INT8_PT_I8PV=1", "-DQMHA_FOLD_PK=1"]
-
-    def compile_one(n):
-        cmd = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "--offload-arch=gfx950", *flags,
-               "-I", os.path.join(ROOT, "include"), "-I", csrc, "-c", os.path.join(csrc, n), "-o", str(tmp_path / (n + ".o"))]
-        return n, subprocess.run(cmd, capture_output=True, text=True, timeout=580)
-
-    with cf.ThreadPoolExecutor(2) as ex:
-        for n, r in ex.map(compile_one, ["qmha_fa_int8.hip", "qmha_prepass.hip"]):
-            assert r.returncode == 0, n + ": " + r.stderr[-3000:]

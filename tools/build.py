@@ -7,6 +7,7 @@
 Outputs (in-tree, git-ignored, shipped to the GPU box with the snapshot):
     quantizedmha_amd/lib/libqmha.so                 all C-ABI entry points (include/launchers.h)
     quantizedmha_amd/lib/libqmha_<variant>.so       `solve` bound to one kernel (reference Makefile KERNEL=)
+    quantizedmha_amd/lib/libqmha_probe.so           bench.py's in-kernel clock probe (qmha_clock_probe.hip)
     quantizedmha_amd/bin/qmha_profile               HIP C++ host driver (reference drivers/main.cu)
     quantizedmha_amd/lib/torch_ext<EXT_SUFFIX>      compiled pybind module `torch_ext` (reference
                                                     extensions/torch/torch_ext.cpp), linked to libqmha.so
@@ -39,7 +40,7 @@ KERNEL_SOURCES = ["qmha_fa_int8.hip", "qmha_fa_f16.hip", "qmha_prepass.hip", "qm
 # (tools/ablation/qmha_fa_int8_ablation.hip).  Int8 ablation builds compile the production source.
 VARIANTS = {"fa": 0, "fa_tc_v1a": 1, "fa_tc_int8_b": 2, "unfused": 3, "fa_mfma": 4, "fa_tc_int8_pt": 5}
 DRIVER_SOURCES = ["driver/main.cpp", "driver/data.cpp", "driver/verify.cpp"]
-HEADERS = ["qmha_common.hpp", "qmha_fused.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
+HEADERS = ["qmha_common.hpp", "qmha_kernels.hpp", "driver/data.h", "driver/verify.h"]
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
                 "-Wno-unused-variable", "-Wno-unused-lambda-capture", "-munsafe-fp-atomics",
@@ -140,6 +141,10 @@ def build(jobs=8, verbose=True):
         out = os.path.join(LIB, f"libqmha_{name}.so")
         if newer(out, [o, libqmha]):
             run([HIPCC, "-shared", "-fPIC", "-o", out, o, "-L", LIB, "-lqmha", "-Wl,-rpath,$ORIGIN"])
+    probe = os.path.join(LIB, "libqmha_probe.so")  # bench.py's clock probe (not part of the C-ABI library)
+    po = compile_one("qmha_clock_probe.hip")
+    if newer(probe, [po]):
+        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", probe, po])
     text = build_torch_ext(libqmha)
     driver = os.path.join(BIN, "qmha_profile")
     if newer(driver, drv_objs + [libqmha]):

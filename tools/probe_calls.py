@@ -37,12 +37,6 @@ def main():
     lib = _lib.load()
     if os.environ.get("QMHA_OVERLAP"):  # batch chunks with the pre-pass of chunk c+1 beside chunk c's main kernel
         lib.qmha_set_overlap_chunks(int(os.environ["QMHA_OVERLAP"]))
-    if os.environ.get("QMHA_FUSED"):  # 0: the int8 pre-pass as its own launch (default); 1: in the main kernel
-        lib.qmha_debug_set_int8_fused(int(os.environ["QMHA_FUSED"]))
-    if os.environ.get("QMHA_F16_FUSED"):  # fa_tc_v1a: 0 the conversion pre-pass as its own launch, 1 in the main kernel
-        lib.qmha_debug_set_f16_fused(int(os.environ["QMHA_F16_FUSED"]))
-    if os.environ.get("QMHA_FUSED_ABLATE"):  # parts of the fused kernel switched off (results wrong: timing only)
-        lib.qmha_debug_set_int8_fused_ablate(int(os.environ["QMHA_FUSED_ABLATE"]))
     vid = _lib.variant_id(a.variant)
     dev = torch.device("cuda:0")
     B, H, N, d = a.B, a.H, a.N, a.d
