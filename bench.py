@@ -58,7 +58,45 @@ def max_over_ranks(x, dev):
     return float(t.item())
 
 
-def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=True, dry_run=False, uniform=False):
+class SysfsSampler:
+    """Samples this GPU's hwmon clock and power (sysfs file reads on a host thread, no GPU calls) every
+    `period` seconds while the timed calls run: the clock the main kernel actually ran at, beside the
+    in-kernel probe's (round-5 VERDICT item 2)."""
+
+    def __init__(self, hwmon, period=0.002):
+        self.files = {k: os.path.join(hwmon, f) for k, f in (("sclk_mhz", "freq1_input"), ("power_w", "power1_input"))
+                      if hwmon and os.path.exists(os.path.join(hwmon, f))}
+        self.period, self.samples, self._stop = period, {k: [] for k in self.files}, None
+
+    def __enter__(self):
+        import threading
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                for k, path in self.files.items():
+                    v = _read(path)
+                    if v and v.isdigit():
+                        self.samples[k].append(int(v) * 1e-6)
+                self._stop.wait(self.period)
+        self._t = threading.Thread(target=loop, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
+
+    def summary(self):
+        out = {}
+        for k, v in self.samples.items():
+            if v:
+                out[k] = {"mean": round(sum(v) / len(v), 1), "min": round(min(v), 1), "max": round(max(v), 1), "n": len(v)}
+        return out
+
+
+def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=True, dry_run=False, uniform=False,
+                sampler=None):
     """Time `steps` qmha_solve_ex calls on this rank's own shard (B sequences), bracketed by a
     barrier + device synchronisation on both sides; the max over ranks is returned.
     dry_run (CPU, gloo; launcher/rendezvous plumbing only): the step is a tensor copy.
@@ -96,13 +134,16 @@ def run_variant(variant, B, H, N, d, steps, warmup, dev, rank, world, profile=Tr
     if dist.is_initialized():
         dist.barrier()
     _sync(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    _sync(dev)
+    import contextlib
+    with (sampler or contextlib.nullcontext()):
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        _sync(dev)
+        t1 = time.perf_counter()
     if dist.is_initialized():
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    elapsed = max_over_ranks(t1 - t0, dev)
     import ctypes
     main_ms, pre_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
     if lib is not None:
@@ -472,7 +513,8 @@ def main():
     if not a.no_siblings and not dry and world == 1:
         side["quantize_int8"] = time_quantize_int8(B, H, N, d, dev)
 
-    r = run_variant(a.variant, B, H, N, d, a.steps, a.warmup, dev, rank, world, dry_run=dry)
+    sampler = None if dry else SysfsSampler(device_state(dev).get("hwmon"))
+    r = run_variant(a.variant, B, H, N, d, a.steps, a.warmup, dev, rank, world, dry_run=dry, sampler=sampler)
     total_flops = flops(B, H, N, d) * world
     value = total_flops / r["elapsed_s"] * a.steps / 1e12
     peak = PEAKS.get(a.variant, INT8_PEAK_TOPS)
@@ -527,6 +569,7 @@ def main():
         dstate = device_state(dev)
         ids = isa_ids(a.variant, d)
         res["device"] = dstate
+        res["sysfs_during_timed_calls"] = sampler.summary() if sampler else None
         res["clock_probe"] = probe
         res["power_cap_w"] = dstate.get("power_cap_w")
         res["isa_sha16"] = ids.get("main", {}).get("isa_sha16")
