@@ -582,6 +582,9 @@ def main():
             res["cycles_per_tile"] = round(r["main_kernel_ms"] * 1e-3 * ghz * 1e9 / tiles, 1)
             res["roofline"]["cycles_per_tile"] = res["cycles_per_tile"]
             res["roofline"]["tiles_per_simd"] = tiles
+            # clock-free form: the tile's time in units of the probe's own unit time on the same box (the
+            # ratio of two wall times; DESIGN.md 7.1: constant to +-0.3 % over five boxes)
+            res["probe_units_per_tile"] = round(r["main_kernel_ms"] * 1e6 / tiles / probe["ns_per_unit_per_simd"], 4)
     if dist.is_initialized():
         ag_ms = time_allgather(r["O"], max(3, a.steps // 2), dev, world)
         sg_ms = time_solve_gather(a.variant, r["inputs"], H, d, max(3, a.steps // 2), dev, world,
