@@ -39,7 +39,8 @@ def lib():
             build()
         L = ctypes.CDLL(path)
         i, f, sz, l = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_long
-        for name in ("oracle_cpu_attention", "oracle_fa_int8", "oracle_fa_fp16", "oracle_fa_fp32", "oracle_fa_int8_pt"):
+        for name in ("oracle_cpu_attention", "oracle_fa_int8", "oracle_fa_fp16", "oracle_fa_fp32", "oracle_fa_int8_pt",
+                     "oracle_fa_fp16_lazy"):
             fn = getattr(L, name)
             fn.argtypes = [_f32p, _f32p, _f32p, _f32p, i, i, i, i, i]
             fn.restype = None
@@ -121,6 +122,12 @@ def fa_int8_pt(Q, K, V, d_model, h, nthreads=0):
 def fa_fp16(Q, K, V, d_model, h, nthreads=0):
     """mha_kernels/fa_tc_v1a.cu."""
     return _run4(lib().oracle_fa_fp16, Q, K, V, d_model, h, nthreads)
+
+
+def fa_fp16_lazy(Q, K, V, d_model, h, nthreads=0):
+    """The fp16 GPU kernel's own contract (r06): fa_tc_v1a in base 2 with a lazy softmax base (DESIGN.md 3);
+    the tests pin the kernel to it tightly and to fa_fp16 (the reference) within the fp16 bound."""
+    return _run4(lib().oracle_fa_fp16_lazy, Q, K, V, d_model, h, nthreads)
 
 
 def fa_fp32(Q, K, V, d_model, h, nthreads=0):

@@ -610,6 +610,86 @@ void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,
     parallel_for((long)B * h * (N / GROUP), nthreads, fa_fp16_item, &c);
 }
 
+/* The fp16 GPU kernel's own contract (r06): fa_tc_v1a's arithmetic with the softmax in
+ * base 2 (x = S * (1/sqrtf(d)) * log2 e, exp2) and a LAZY base: p = exp2(x - m) against a per-row base m
+ * (m0 = 0) that moves to the tile's row max only when that max passes it by more than 8 log2 units;
+ * then O and l are scaled by exp2(m_old - m_new).  The reference (oracle_fa_fp16 above) moves m on every
+ * tile; the two differ only in the rounding of half(p).  Used by the tests to pin the kernel tightly
+ * (the reference bound is checked against oracle_fa_fp16). */
+static void fa_fp16_lazy_item(long item, void *vctx) {
+    fa_ctx *c = (fa_ctx *)vctx;
+    int N = c->N, dm = c->d_model, dh = dm / c->h, G = N / GROUP;
+    long bh = item / G;
+    int g = (int)(item % G);
+    int b = (int)(bh / c->h), head = (int)(bh % c->h);
+    const float c_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f; /* the kernel's score constant */
+    const float rebase = 8.0f;
+    const float *Qb = c->Q + (size_t)b * N * dm + head * dh;
+    const float *Kb = c->K + (size_t)b * N * dm + head * dh;
+    const float *Vb = c->V + (size_t)b * N * dm + head * dh;
+    float *q = (float *)malloc(sizeof(float) * GROUP * dh);
+    float *kt = (float *)malloc(sizeof(float) * GROUP * dh);
+    float *vv = (float *)malloc(sizeof(float) * GROUP * dh);
+    float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
+    float l[GROUP], m[GROUP], s[GROUP][GROUP], ph[GROUP][GROUP];
+    for (int r = 0; r < GROUP; ++r) {
+        l[r] = 0.0f;
+        m[r] = 0.0f;
+        for (int d = 0; d < dh; ++d)
+            q[r * dh + d] = oracle_f16_to_f32(oracle_f32_to_f16(Qb[(size_t)(g * GROUP + r) * dm + d]));
+    }
+    for (int t = 0; t < G; ++t) {
+        for (int j = 0; j < GROUP; ++j)
+            for (int d = 0; d < dh; ++d) {
+                kt[j * dh + d] = oracle_f16_to_f32(oracle_f32_to_f16(Kb[(size_t)(t * GROUP + j) * dm + d]));
+                vv[j * dh + d] = oracle_f16_to_f32(oracle_f32_to_f16(Vb[(size_t)(t * GROUP + j) * dm + d]));
+            }
+        for (int r = 0; r < GROUP; ++r)
+            for (int j = 0; j < GROUP; ++j) {
+                float acc = 0.0f;
+                for (int d = 0; d < dh; ++d) acc = fmaf(q[r * dh + d], kt[j * dh + d], acc);
+                s[r][j] = acc; /* raw S: the kernel scales inside the exponent */
+            }
+        for (int r = 0; r < GROUP; ++r) {
+            float mx = s[r][0];
+            for (int j = 1; j < GROUP; ++j) mx = fmaxf(mx, s[r][j]);
+            const float xm = mx * c_log2;
+            if (xm > m[r] + rebase) {
+                const float alpha = exp2f(m[r] - xm);
+                l[r] *= alpha;
+                for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
+                m[r] = xm;
+            }
+            float lane[GROUP];
+            for (int j = 0; j < GROUP; ++j) {
+                const float p = exp2f(fmaf(s[r][j], c_log2, -m[r]));
+                lane[j] = p;
+                ph[r][j] = oracle_f16_to_f32(oracle_f32_to_f16(p));
+            }
+            l[r] += xor_tree_sum32(lane);
+        }
+        for (int r = 0; r < GROUP; ++r)
+            for (int d = 0; d < dh; ++d) {
+                float acc = 0.0f;
+                for (int j = 0; j < GROUP; ++j) acc = fmaf(ph[r][j], vv[j * dh + d], acc);
+                O[r * dh + d] = acc + O[r * dh + d];
+            }
+    }
+    float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * dm + head * dh;
+    for (int r = 0; r < GROUP; ++r)
+        for (int d = 0; d < dh; ++d) out[(size_t)r * dm + d] = (l[r] > 1e-10f) ? O[r * dh + d] / l[r] : 0.0f;
+    free(q);
+    free(kt);
+    free(vv);
+    free(O);
+}
+
+void oracle_fa_fp16_lazy(const float *Q, const float *K, const float *V, float *out,
+                         int B, int N, int d_model, int h, int nthreads) {
+    fa_ctx c = {Q, K, V, out, B, N, d_model, h};
+    parallel_for((long)B * h * (N / GROUP), nthreads, fa_fp16_lazy_item, &c);
+}
+
 /* ------------------------------------------------------------------------- */
 /* FP32 scalar: mha_kernels/fa.cu                                             */
 /* ------------------------------------------------------------------------- */

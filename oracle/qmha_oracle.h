@@ -76,6 +76,10 @@ void oracle_fa_int8_pt(const float *Q, const float *K, const float *V, float *ou
  * P stored as half(p), m0 = 0, epilogue guard 1e-10. */
 void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,
                     int B, int N, int d_model, int h, int nthreads);
+/* The fp16 GPU kernel's contract (r06): the above in base 2 with a lazy softmax base (moves only when a
+ * row's tile max passes it by > 8 log2 units); differs from oracle_fa_fp16 in the rounding of half(p). */
+void oracle_fa_fp16_lazy(const float *Q, const float *K, const float *V, float *out,
+                         int B, int N, int d_model, int h, int nthreads);
 
 /* mha_kernels/fa.cu:24-400 -- fp32 scalar FlashAttention, fmaf dot products
  * (nvcc contracts acc += a*b), m0 = 0, Bc = 32, epilogue guard 1e-10. */

@@ -714,6 +714,24 @@ def test_c5_global_batch_on_one_gpu(dev, oracle_mod):
     torch.cuda.empty_cache()
 
 
+FP16_LAZY_TOL = 4e-5  # GPU vs its own contract (oracle fa_fp16_lazy): v_exp_f32 vs libm exp2f ulps flip half(p)
+
+
+@pytest.mark.parametrize("N,d", [(32, 64), (64, 32), (96, 128), (256, 64), (1024, 64), (2048, 128), (4096, 32)])
+@pytest.mark.parametrize("dist", ["normal", "uniform"])
+def test_fp16_lazy_base_contract(dev, oracle_mod, N, d, dist):
+    """The fp16 kernel's lazy softmax base (r06): pinned tightly to its own restatement
+    (oracle fa_fp16_lazy) and held to the 2e-4 fp16 bound against the reference's algorithm (fa_fp16)."""
+    h = 2
+    Q, K, V = rand_inputs(300 + N + d, 2, N, h * d, dist)
+    out = run("fa_tc_v1a", Q, K, V, h * d, h, dev)
+    lazy = oracle_mod.fa_fp16_lazy(Q, K, V, h * d, h)
+    err = float(np.abs(out.astype(np.float64) - lazy).max())
+    parity_log.record(f"test_fp16_lazy_base_contract[{N}-{d}-{dist}]", "fa_tc_v1a (vs lazy)", err, 0.0, FP16_LAZY_TOL)
+    assert err <= FP16_LAZY_TOL, err
+    assert_parity("fa_tc_v1a", out, oracle_mod.fa_fp16(Q, K, V, h * d, h))
+
+
 def test_c3_fp16_full_config_all_heads(dev, oracle_mod):
     """BASELINE C3 (fa_tc_v1a, fp16 MFMA, B16 H16 N4096 d64) at its own workload: the whole
     call on the GPU, ALL 256 (batch, head) slices against oracle fa_fp16 at 2e-4 (fa_tc_v1a.cu:222-413)."""

@@ -74,6 +74,16 @@ def test_fa_fp16_within_reference_tolerance(oracle_mod, case):
 
 
 @pytest.mark.parametrize("case", ["medium", "large", "huge_1024"])
+def test_fa_fp16_lazy_within_reference_tolerance(oracle_mod, case):
+    """The fp16 kernel's own contract (lazy softmax base): inside the reference's verify tolerance
+    against the goldens, and within the 2e-4 fp16 parity bound of the reference's algorithm (fa_fp16)."""
+    N, dm, h, Q, K, V, O = load_case(case)
+    out = oracle_mod.fa_fp16_lazy(Q, K, V, dm, h)
+    assert oracle_mod.verify_results(out, O, 1e-3, 1e-3) == -1
+    assert np.abs(out - oracle_mod.fa_fp16(Q, K, V, dm, h)).max() <= 2e-4
+
+
+@pytest.mark.parametrize("case", ["medium", "large", "huge_1024"])
 def test_fa_fp32_close_to_golden(oracle_mod, case):
     N, dm, h, Q, K, V, O = load_case(case)
     out = oracle_mod.fa_fp32(Q, K, V, dm, h)
