@@ -448,6 +448,7 @@ void oracle_quantize_heads_pt(const float *X, int B, int N, int d_model, int h, 
     parallel_for((long)B * h, 0, quantize_tensor_item, &c);
 }
 
+#define PT_REBASE_NATS (4.0f * 0.69314718055994531f) /* the kernel's kPtRebase = 4 log2 units */
 static void fa_int8_pt_item(long item, void *vctx) {
     int8_ctx *c = (int8_ctx *)vctx;
     int N = c->N, dh = c->d_model / c->h, G = N / GROUP;
@@ -476,8 +477,11 @@ static void fa_int8_pt_item(long item, void *vctx) {
                 s[r][j] = deq * inv_sqrt_d;
             }
         for (int r = 0; r < GROUP; ++r) {
-            float m_new = m_prev[r];
-            for (int j = 0; j < GROUP; ++j) m_new = fmaxf(m_new, s[r][j]);
+            /* lazy base (r06): the row's base moves to the tile's row max only when that max passes it by
+             * more than 4 log2 units (4 ln 2 here), so p <= 16 and Pi <= 2032 */
+            float rowmax = s[r][0];
+            for (int j = 1; j < GROUP; ++j) rowmax = fmaxf(rowmax, s[r][j]);
+            const float m_new = rowmax > m_prev[r] + PT_REBASE_NATS ? rowmax : m_prev[r];
             float lane[GROUP];
             for (int j = 0; j < GROUP; ++j) {
                 s[r][j] = expf(s[r][j] - m_new);
@@ -490,8 +494,8 @@ static void fa_int8_pt_item(long item, void *vctx) {
             m_prev[r] = m_new;
             int Pi[GROUP];
             for (int j = 0; j < GROUP; ++j) {
-                float rr = rintf(s[r][j] * 127.0f); /* static P scale 1/127; p in [0, 1] */
-                Pi[j] = rr != rr ? 0 : (int)fminf(rr, 127.0f);
+                float rr = rintf(s[r][j] * 127.0f); /* static P scale 1/127; p in [0, 16] */
+                Pi[j] = rr != rr ? 0 : (int)fminf(rr, 2047.0f);
             }
             for (int d = 0; d < dh; ++d) {
                 int32_t acc = 0;

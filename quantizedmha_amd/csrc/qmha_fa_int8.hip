@@ -43,6 +43,9 @@ namespace qmha {
 
 // log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
 static constexpr float kLog2e = 1.4426950408889634f;
+// The per-tensor mode's lazy softmax base: p <= 2^4, so Pi = rint(127 p f) <= 2032 stays
+// below 2048, where the magic-number Pi bits are still the f16 encoding of Pi * 2^-24.
+static constexpr float kPtRebase = 4.0f;
 
 // A NaN in the caller's Q becomes 0 before the quantiser sees it, explicitly (integer test on the
 // bits): the reference's fmaxf drops a NaN from the group absmax and __float2int_rn maps it to 0
@@ -521,7 +524,11 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const int mxi = half_swap_max_i(tree_max16_i(s));
         if constexpr (!PT) c = __int_as_float((__float_as_int(c) + 2) & ~3);
         const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;  // exact float(S_max)
-        h_m = fmaxf(m_run, sfmax * c);
+        const float xm = sfmax * c;
+        if constexpr (PT)  // lazy base (r06): moves only when the row max passes it by > kPtRebase
+            h_m = xm > m_run + kPtRebase ? xm : m_run;
+        else
+            h_m = fmaxf(m_run, xm);
         h_k = fmaf(c, QMHA_MAGIC_RNE, h_m);
         const float delta = fmaf(c, -QMHA_MAGIC_RNE, h_k) - h_m;  // m_eff - m, exact
         h_f = fmaf(delta, 0.69314718055994531f, 1.0f);

@@ -223,11 +223,12 @@ def _np_fa_int8_pt(Q, K, V, h):
             for t in range(N // 32):
                 cols = slice(32 * t, 32 * t + 32)
                 S = (Qi[rows] @ Ki[cols].T).astype(f) * sQ * sK * inv
-                m_new = np.maximum(m, S.max(axis=1))
+                rowmax = S.max(axis=1)  # lazy base (r06): moves only past base + 4 log2 units
+                m_new = np.where(rowmax > m + f(4.0) * f(np.log(2.0)), rowmax, m).astype(f)
                 p = np.exp(S - m_new[:, None]).astype(f)
                 alpha = np.exp(m - m_new).astype(f)
                 l = alpha * l + p.sum(axis=1, dtype=f)
-                Pi = np.minimum(np.rint(p * f(127.0)), 127).astype(np.int32)
+                Pi = np.minimum(np.rint(p * f(127.0)), 2047).astype(np.int32)
                 O = O * alpha[:, None] + (Pi @ Vi[cols]).astype(f)
                 m = m_new
             out[rows, sl] = np.where(l[:, None] > 1e-20, O * (sV / f(127.0)) / l[:, None], 0)
