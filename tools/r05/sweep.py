@@ -2,8 +2,7 @@
 """Extended parity sweep on the GPU (evidence beyond the pytest suite, not part of it): random shapes
 (B 1..6, N = 32 * (1..96), H 1..8, d in {32, 64, 128}, N(0, 0.5^2) or U[0, 1) inputs) through every
 fused-attention variant against the oracle, at the suite's criteria (tests/test_gpu_parity.py
-assert_parity); for fa_tc_int8_b and fa_tc_v1a also the one-launch opt-ins, which must equal the default
-call bit for bit.  Test infrastructure: the oracle is the checker.
+assert_parity), fa_tc_v1a also against its lazy-base contract (oracle fa_fp16_lazy, FP16_LAZY_TOL).  (Until r05 it also compared the one-launch opt-ins, removed in r06.)  Test infrastructure: the oracle is the checker.
     python tools/r05/sweep.py [--n 200] [--seed 5] [--variants fa_tc_int8_pt]"""
 import argparse
 import os
@@ -17,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from oracle import oracle as oracle_mod  # noqa: E402
 from quantizedmha_amd import _lib, torch_ext  # noqa: E402
-from tests.test_gpu_parity import INT8_TOL_TIGHT, INT8_FLIP_FRAC, INT8_FLIP_FRAC_PT, TOL_ORACLE, int8_tol  # noqa: E402
+from tests.test_gpu_parity import FP16_LAZY_TOL, INT8_TOL_TIGHT, INT8_FLIP_FRAC, INT8_FLIP_FRAC_PT, TOL_ORACLE, int8_tol  # noqa: E402
 
 VARIANTS = ("fa_tc_int8_b", "fa_tc_int8_pt", "fa_tc_v1a", "fa")
 
@@ -78,9 +77,13 @@ def main():
                 print(f"  {v}: {int(big.sum())} elements above {INT8_TOL_TIGHT} in {len(rows)} (batch, row, head) "
                       f"rows: {rows[:12]}; per row: {[int(big[r].sum()) for r in rows[:12]]}", flush=True)
             worst[v] = max(worst[v], e)
-            fused = ""  # (r05: the one-launch opt-ins were compared here; removed in r06)
+            if v == "fa_tc_v1a":  # since r06 also against the kernel's own lazy-base contract (oracle fa_fp16_lazy)
+                el = float(np.abs(out.cpu().numpy().astype(np.float64) - oracle_mod.fa_fp16_lazy(Q, K, V, dm, H, nthreads=16)).max())
+                worst["fa_tc_v1a (vs lazy)"] = max(worst.get("fa_tc_v1a (vs lazy)", 0.0), el)
+                ok = ok and el <= FP16_LAZY_TOL
+                line.append(f"[lazy {el:.2e}]")
             fails += not ok
-            line.append(f"{v} {e:.2e}/{frac:.1e}{fused}{'' if ok else ' FAIL'}")
+            line.append(f"{v} {e:.2e}/{frac:.1e}{'' if ok else ' FAIL'}")
         print(" ".join(line), flush=True)
     print(f"{a.n} shapes, {fails} failures, {time.time() - t0:.0f} s; worst max|gpu - oracle|: " +
           ", ".join(f"{v} {e:.2e}" for v, e in worst.items()), flush=True)
