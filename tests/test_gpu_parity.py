@@ -732,6 +732,35 @@ def test_fp16_lazy_base_contract(dev, oracle_mod, N, d, dist):
     assert_parity("fa_tc_v1a", out, oracle_mod.fa_fp16(Q, K, V, h * d, h))
 
 
+@pytest.mark.parametrize("variant,T", [("fa_tc_int8_pt", 4.0), ("fa_tc_v1a", 8.0)])
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_lazy_base_staircase(dev, oracle_mod, variant, T, d):
+    """The lazy softmax base at its limit (r06): every 32-key tile's row maxima sit
+    0.95 T log2 units above the previous tile's (T = 4 per-tensor, 8 fp16), so the base lags by up to
+    0.95 T on every other tile and moves on the next -- the per-tensor Pi reach ~2^3.8 * 127 = 1773 of the
+    2047 an f16 subnormal holds, the fp16 P ~2^7.6.  Checked against the kernel's own contract (the
+    per-tensor oracle is lazy; oracle fa_fp16_lazy) and, for fp16, against the reference's algorithm."""
+    B, N, h = 2, 512, 2
+    dm = h * d
+    rng = np.random.default_rng(int(T) * 1000 + d)
+    Q = (0.5 + 0.01 * rng.standard_normal((B, N, dm))).astype(np.float32)
+    # log2-unit score of a key at level a: 0.5 * a * d / sqrt(d) * log2(e)
+    step = 0.95 * T / (0.5 * np.sqrt(d) * np.log2(np.e))
+    level = np.repeat(np.arange(N // 32) * step, 32)[None, :, None]
+    K = (level + 0.01 * rng.standard_normal((B, N, dm))).astype(np.float32)
+    V = rng.standard_normal((B, N, dm)).astype(np.float32)
+    out = run(variant, Q, K, V, dm, h, dev)
+    if variant == "fa_tc_int8_pt":
+        assert_parity(variant, out, oracle_mod.fa_int8_pt(Q, K, V, dm, h))
+        return
+    lazy = oracle_mod.fa_fp16_lazy(Q, K, V, dm, h)
+    err = float(np.abs(out.astype(np.float64) - lazy).max())
+    parity_log.record(f"test_lazy_base_staircase[{variant}-{d}]", "fa_tc_v1a (vs lazy)", err, 0.0, FP16_LAZY_TOL)
+    assert err <= FP16_LAZY_TOL, err
+    # few dominant keys per row: one exp2-vs-expf ulp flips half(p), as in test_growing_scores_reanchor
+    assert_parity(variant, out, oracle_mod.fa_fp16(Q, K, V, dm, h), scale=5.0)
+
+
 def test_c3_fp16_full_config_all_heads(dev, oracle_mod):
     """BASELINE C3 (fa_tc_v1a, fp16 MFMA, B16 H16 N4096 d64) at its own workload: the whole
     call on the GPU, ALL 256 (batch, head) slices against oracle fa_fp16 at 2e-4 (fa_tc_v1a.cu:222-413)."""
