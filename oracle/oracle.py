@@ -115,7 +115,8 @@ def fa_int8(Q, K, V, d_model, h, nthreads=0):
 
 def fa_int8_pt(Q, K, V, d_model, h, nthreads=0):
     """Per-tensor int8 mode (fa_tc_int8_pt; not a reference kernel: BASELINE.json's "per-tensor
-    Q/K/V quant", SURVEY 0.2's optional flag): per-head-slice scales, static P scale 1/127."""
+    Q/K/V quant", SURVEY 0.2's optional flag): per-head-slice scales, static P scale 1/127, lazy softmax
+    base, stated in base 2 with the kernel's 22-bit score constant (qmha_oracle.c)."""
     return _run4(lib().oracle_fa_int8_pt, Q, K, V, d_model, h, nthreads)
 
 

@@ -422,11 +422,15 @@ void oracle_fa_int8(const float *Q, const float *K, const float *V, float *out,
  * ("a per-tensor mode may be offered as an extra flag").  Same quantiser
  * (fa_tc_int8_b.cu:33-152) applied to each head's whole [N, d] slice -- the matrix the
  * reference's launch<> extracts per head (include/launchers.h:42-52) -- and P quantised with
- * the static scale 1/127 (p = exp(s - m) lies in [0, 1]), so the P@V products of every tile
- * share one unit and O accumulates as the int32 sums, rescaled by alpha only:
- *   s = (float)(Qi.Ki)[int32] * sQ * sK * (1/sqrt(d)),  online softmax as fa_tc_int8_b (m0 = 0),
- *   Pi = rint(p * 127),  O = alpha * O + (float)(Pi.Vi)[int32],
- *   out = l > 1e-20 ? (O * (sV / 127)) / l : 0.                                  */
+ * the static scale 1/127, so the P@V products of every tile share one unit and O accumulates as
+ * the int32 sums, rescaled by alpha only.  The contract is stated in base 2 with the score
+ * constant the kernel uses (r06; this mode has no reference numerics to follow):
+ *   c = RN22(sQ * RN(RN(1/sqrt(d)) * log2 e) * sK)   (float products; RN22: 22 significant bits)
+ *   x = RN(S * c - m)   (S the int32 Q.K, one rounding: the kernel's fused multiply-add),
+ *   row max xm = RN(S_max * c); lazy base m: moves to xm only when xm > m + 4 (m0 = 0),
+ *   p = 2^x in [0, 16],  Pi = min(rint(127 p), 2047),  alpha = 2^(m_old - m_new),
+ *   l = alpha l + sum(p),  O = alpha O + (float)(Pi.Vi)[int32],
+ *   out = l > 1e-20 ? (O * (sV / 127)) / l : 0.                                   */
 /* ------------------------------------------------------------------------- */
 typedef struct {
     const float *X;
@@ -448,16 +452,28 @@ void oracle_quantize_heads_pt(const float *X, int B, int N, int d_model, int h, 
     parallel_for((long)B * h, 0, quantize_tensor_item, &c);
 }
 
-#define PT_REBASE_NATS (4.0f * 0.69314718055994531f) /* the kernel's kPtRebase = 4 log2 units */
+#define PT_REBASE_LOG2 4.0f /* the kernel's kPtRebase */
+/* the kernel's score constant (qmha_fa_int8.hip: c_log2 on the host, cq, c_pt) */
+static float pt_score_constant(float sQ, float sK, int dh) {
+    const float c_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
+    const float cq = sQ * c_log2;
+    const float c = cq * sK;
+    uint32_t u;
+    memcpy(&u, &c, 4);
+    u = (u + 2u) & ~3u; /* 22 significant bits, ties away from zero (c >= 0) */
+    float r;
+    memcpy(&r, &u, 4);
+    return r;
+}
 static void fa_int8_pt_item(long item, void *vctx) {
     int8_ctx *c = (int8_ctx *)vctx;
     int N = c->N, dh = c->d_model / c->h, G = N / GROUP;
     long bh = item / G;
     int g = (int)(item % G);
     int b = (int)(bh / c->h), head = (int)(bh % c->h);
-    const float inv_sqrt_d = 1.0f / sqrtf((float)dh);
     const int8_t *Qg = c->Qi + ((size_t)bh * N + (size_t)g * GROUP) * dh;
-    const float sQ = c->sQ[bh], sK = c->sK[bh], sV = c->sV[bh];
+    const float sV = c->sV[bh];
+    const float cc = pt_score_constant(c->sQ[bh], c->sK[bh], dh);
 
     float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
     float l[GROUP], m_prev[GROUP];
@@ -465,7 +481,7 @@ static void fa_int8_pt_item(long item, void *vctx) {
         l[r] = 0.0f;
         m_prev[r] = 0.0f; /* m0 = 0, as fa_tc_int8_b.cu:402 */
     }
-    float s[GROUP][GROUP];
+    int32_t S[GROUP][GROUP];
     for (int t = 0; t < G; ++t) {
         const int8_t *Kt = c->Ki + ((size_t)bh * N + (size_t)t * GROUP) * dh;
         const int8_t *Vt = c->Vi + ((size_t)bh * N + (size_t)t * GROUP) * dh;
@@ -473,28 +489,26 @@ static void fa_int8_pt_item(long item, void *vctx) {
             for (int j = 0; j < GROUP; ++j) {
                 int32_t acc = 0;
                 for (int k = 0; k < dh; ++k) acc += (int32_t)Qg[r * dh + k] * (int32_t)Kt[j * dh + k];
-                float deq = (float)acc * sQ * sK;
-                s[r][j] = deq * inv_sqrt_d;
+                S[r][j] = acc;
             }
         for (int r = 0; r < GROUP; ++r) {
             /* lazy base (r06): the row's base moves to the tile's row max only when that max passes it by
-             * more than 4 log2 units (4 ln 2 here), so p <= 16 and Pi <= 2032 */
-            float rowmax = s[r][0];
-            for (int j = 1; j < GROUP; ++j) rowmax = fmaxf(rowmax, s[r][j]);
-            const float m_new = rowmax > m_prev[r] + PT_REBASE_NATS ? rowmax : m_prev[r];
-            float lane[GROUP];
-            for (int j = 0; j < GROUP; ++j) {
-                s[r][j] = expf(s[r][j] - m_new);
-                lane[j] = s[r][j];
-            }
-            float sum_new = xor_tree_sum32(lane);
-            float alpha = expf(m_prev[r] - m_new);
+             * more than 4 log2 units, so p <= 16 and Pi <= 2032 */
+            int32_t smax = S[r][0];
+            for (int j = 1; j < GROUP; ++j) smax = S[r][j] > smax ? S[r][j] : smax;
+            const float xm = (float)smax * cc;
+            const float m_new = xm > m_prev[r] + PT_REBASE_LOG2 ? xm : m_prev[r];
+            float p[GROUP];
+            for (int j = 0; j < GROUP; ++j) /* S * cc is exact in double (< 53 bits): one rounding */
+                p[j] = exp2f((float)((double)S[r][j] * (double)cc - (double)m_new));
+            float sum_new = xor_tree_sum32(p);
+            float alpha = exp2f(m_prev[r] - m_new);
             l[r] = fmaf(alpha, l[r], sum_new);
             for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
             m_prev[r] = m_new;
             int Pi[GROUP];
             for (int j = 0; j < GROUP; ++j) {
-                float rr = rintf(s[r][j] * 127.0f); /* static P scale 1/127; p in [0, 16] */
+                float rr = rintf(p[j] * 127.0f); /* static P scale 1/127; p in [0, 16] */
                 Pi[j] = rr != rr ? 0 : (int)fminf(rr, 2047.0f);
             }
             for (int d = 0; d < dh; ++d) {

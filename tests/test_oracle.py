@@ -201,8 +201,17 @@ def test_int8_pt_quantiser_semantics(oracle_mod):
     assert np.array_equal(Yi_pt[:, 0], Yi_pb[:, 0])
 
 
+def _pt_score_constant(sQ, sK, d):
+    """The kernel's base-2 score constant: RN22(sQ * RN(RN(1/sqrt(d)) * log2 e) * sK) in float32."""
+    f = np.float32
+    c_log2 = (f(1.0) / np.sqrt(f(d))) * f(1.4426950408889634)
+    c = np.array([(f(sQ) * c_log2) * f(sK)], np.float32).view(np.uint32)
+    return ((c + np.uint32(2)) & np.uint32(0xFFFFFFFC)).view(np.float32)[0]
+
+
 def _np_fa_int8_pt(Q, K, V, h):
-    """numpy restatement of oracle_fa_int8_pt for one sequence (float32 arithmetic throughout)."""
+    """numpy restatement of oracle_fa_int8_pt for one sequence (base 2, the kernel's score constant;
+    float32 arithmetic except x = S * c - m, rounded once from float64 like the kernel's fma)."""
     f = np.float32
     N, dm = Q.shape
     d = dm // h
@@ -212,9 +221,9 @@ def _np_fa_int8_pt(Q, K, V, h):
         qs = []
         for X in (Q, K, V):
             s = np.maximum(f(np.abs(X[:, sl]).max()) / f(127.0), f(1e-8))
-            qs.append((np.clip(np.rint(X[:, sl] * (f(1.0) / s)), -128, 127).astype(np.int32), s))
+            qs.append((np.clip(np.rint(X[:, sl] * (f(1.0) / s)), -128, 127).astype(np.int64), s))
         (Qi, sQ), (Ki, sK), (Vi, sV) = qs
-        inv = f(1.0) / np.sqrt(f(d))
+        c = _pt_score_constant(sQ, sK, d)
         for g in range(N // 32):
             rows = slice(32 * g, 32 * g + 32)
             O = np.zeros((32, d), f)
@@ -222,13 +231,14 @@ def _np_fa_int8_pt(Q, K, V, h):
             m = np.zeros(32, f)
             for t in range(N // 32):
                 cols = slice(32 * t, 32 * t + 32)
-                S = (Qi[rows] @ Ki[cols].T).astype(f) * sQ * sK * inv
-                rowmax = S.max(axis=1)  # lazy base (r06): moves only past base + 4 log2 units
-                m_new = np.where(rowmax > m + f(4.0) * f(np.log(2.0)), rowmax, m).astype(f)
-                p = np.exp(S - m_new[:, None]).astype(f)
-                alpha = np.exp(m - m_new).astype(f)
+                S = Qi[rows] @ Ki[cols].T
+                xm = S.max(axis=1).astype(f) * c  # lazy base (r06): moves only past base + 4
+                m_new = np.where(xm > m + f(4.0), xm, m).astype(f)
+                x = (S.astype(np.float64) * np.float64(c) - m_new[:, None].astype(np.float64)).astype(f)
+                p = np.exp2(x).astype(f)
+                alpha = np.exp2(m - m_new).astype(f)
                 l = alpha * l + p.sum(axis=1, dtype=f)
-                Pi = np.minimum(np.rint(p * f(127.0)), 2047).astype(np.int32)
+                Pi = np.minimum(np.rint(p * f(127.0)), 2047).astype(np.int64)
                 O = O * alpha[:, None] + (Pi @ Vi[cols]).astype(f)
                 m = m_new
             out[rows, sl] = np.where(l[:, None] > 1e-20, O * (sV / f(127.0)) / l[:, None], 0)
