@@ -630,10 +630,17 @@ void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,
 
 /* The fp16 GPU kernel's own contract (r06): fa_tc_v1a's arithmetic with the softmax in
  * base 2 (x = S * (1/sqrtf(d)) * log2 e, exp2) and a LAZY base: p = exp2(x - m) against a per-row base m
- * (m0 = 0) that moves to the tile's row max only when that max passes it by more than 8 log2 units;
- * then O and l are scaled by exp2(m_old - m_new).  The reference (oracle_fa_fp16 above) moves m on every
- * tile; the two differ only in the rounding of half(p).  Used by the tests to pin the kernel tightly
- * (the reference bound is checked against oracle_fa_fp16). */
+ * (m0 = 0) that moves to the tile's row max only when the p of one of the row's two key halves (the
+ * kernel's lane halves: keys j with bit 2 of j clear / set) sum above 2^12 on that tile; then O and l are
+ * scaled by exp2(m_old - m_new) and the tile's p recomputed.  l is kept per half and summed in the
+ * kernel's order (16-key trees, halves joined at the end).  The reference (oracle_fa_fp16 above) moves m
+ * on every tile; the two differ only in the rounding of half(p).  Used by the tests to pin the kernel
+ * tightly (the reference bound is checked against oracle_fa_fp16). */
+static float tree_sum16_of(const float *p) { /* the kernel's tree_sum16 order */
+    float a = (p[0] + p[1]) + (p[2] + p[3]), b = (p[4] + p[5]) + (p[6] + p[7]);
+    float c = (p[8] + p[9]) + (p[10] + p[11]), d = (p[12] + p[13]) + (p[14] + p[15]);
+    return (a + b) + (c + d);
+}
 static void fa_fp16_lazy_item(long item, void *vctx) {
     fa_ctx *c = (fa_ctx *)vctx;
     int N = c->N, dm = c->d_model, dh = dm / c->h, G = N / GROUP;
@@ -641,7 +648,7 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
     int g = (int)(item % G);
     int b = (int)(bh / c->h), head = (int)(bh % c->h);
     const float c_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f; /* the kernel's score constant */
-    const float rebase = 8.0f;
+    const float cap = 4096.0f; /* the kernel's kLazySumCap */
     const float *Qb = c->Q + (size_t)b * N * dm + head * dh;
     const float *Kb = c->K + (size_t)b * N * dm + head * dh;
     const float *Vb = c->V + (size_t)b * N * dm + head * dh;
@@ -649,9 +656,9 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
     float *kt = (float *)malloc(sizeof(float) * GROUP * dh);
     float *vv = (float *)malloc(sizeof(float) * GROUP * dh);
     float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
-    float l[GROUP], m[GROUP], s[GROUP][GROUP], ph[GROUP][GROUP];
+    float l[GROUP][2], m[GROUP], s[GROUP][GROUP], ph[GROUP][GROUP];
     for (int r = 0; r < GROUP; ++r) {
-        l[r] = 0.0f;
+        l[r][0] = l[r][1] = 0.0f;
         m[r] = 0.0f;
         for (int d = 0; d < dh; ++d)
             q[r * dh + d] = oracle_f16_to_f32(oracle_f32_to_f16(Qb[(size_t)(g * GROUP + r) * dm + d]));
@@ -669,22 +676,27 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
                 s[r][j] = acc; /* raw S: the kernel scales inside the exponent */
             }
         for (int r = 0; r < GROUP; ++r) {
-            float mx = s[r][0];
-            for (int j = 1; j < GROUP; ++j) mx = fmaxf(mx, s[r][j]);
-            const float xm = mx * c_log2;
-            if (xm > m[r] + rebase) {
+            float p[GROUP], ts[2];
+            for (int pass = 0; pass < 2; ++pass) {
+                for (int j = 0; j < GROUP; ++j) p[j] = exp2f(fmaf(s[r][j], c_log2, -m[r]));
+                for (int hh = 0; hh < 2; ++hh) { /* lane half hh holds keys (i & 3) + 8 (i >> 2) + 4 hh */
+                    float ph16[16];
+                    for (int i = 0; i < 16; ++i) ph16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
+                    ts[hh] = tree_sum16_of(ph16);
+                }
+                if (pass == 1 || !(ts[0] > cap || ts[1] > cap)) break;
+                float mx = s[r][0]; /* rebase: the row max, O and l scaled, the tile recomputed */
+                for (int j = 1; j < GROUP; ++j) mx = fmaxf(mx, s[r][j]);
+                const float xm = mx * c_log2;
                 const float alpha = exp2f(m[r] - xm);
-                l[r] *= alpha;
+                l[r][0] *= alpha;
+                l[r][1] *= alpha;
                 for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
                 m[r] = xm;
             }
-            float lane[GROUP];
-            for (int j = 0; j < GROUP; ++j) {
-                const float p = exp2f(fmaf(s[r][j], c_log2, -m[r]));
-                lane[j] = p;
-                ph[r][j] = oracle_f16_to_f32(oracle_f32_to_f16(p));
-            }
-            l[r] += xor_tree_sum32(lane);
+            for (int j = 0; j < GROUP; ++j) ph[r][j] = oracle_f16_to_f32(oracle_f32_to_f16(p[j]));
+            l[r][0] += ts[0];
+            l[r][1] += ts[1];
         }
         for (int r = 0; r < GROUP; ++r)
             for (int d = 0; d < dh; ++d) {
@@ -695,7 +707,10 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
     }
     float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * dm + head * dh;
     for (int r = 0; r < GROUP; ++r)
-        for (int d = 0; d < dh; ++d) out[(size_t)r * dm + d] = (l[r] > 1e-10f) ? O[r * dh + d] / l[r] : 0.0f;
+        for (int d = 0; d < dh; ++d) {
+            const float lr = l[r][0] + l[r][1];
+            out[(size_t)r * dm + d] = (lr > 1e-10f) ? O[r * dh + d] / lr : 0.0f;
+        }
     free(q);
     free(kt);
     free(vv);

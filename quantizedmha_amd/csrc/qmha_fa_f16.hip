@@ -19,8 +19,9 @@
 namespace qmha {
 
 static constexpr float kLog2eH = 1.4426950408889634f;
-// the lazy base's headroom in log2 units: p <= 2^8 keeps half(p) far from the f16 maximum (65504)
-static constexpr float kLazyRebase = 8.0f;
+// the lazy base's cap: a row's base moves only when the p of one of its key halves sum above 2^12 on a
+// tile, so every p stays <= 4096, far from the f16 maximum (65504)
+static constexpr float kLazySumCap = 4096.0f;
 
 
 // ---------------------------------------------------------------------------------------
@@ -149,28 +150,33 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
                                                                 16 * swz_pos<64>(d, 2 * ks + half));
                 }
         }
-        float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);  // max3 chain
+        // Lazy base (r06): p = exp2(x - m_run) against a per-row base m_run (m0 = 0 as the
+        // reference, :290) that moves to the tile's row max only when the tile's p of one of the row's two
+        // key halves (this lane's 16, its partner lane's 16) sum above kLazySumCap -- so every p <= 2^12 and
+        // the O / l rescale of the reference's every-tile alpha (:187-199) happens only then.  The row max is
+        // computed on those tiles only; the sum is the row sum l needs anyway.  The result differs from the
+        // reference's only in the rounding of half(p) (p scaled by 2^delta, not a power of two).
+        float p[16];
 #pragma unroll
-        for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[r]), s[r + 1]);
-        mx = half_swap_max(fmaxf(mx, s[15]));
-        // Lazy base (r06): p = exp2(x - m_run) against a base m_run that moves only when the
-        // tile's row max passes it by more than kLazyRebase log2 units (m0 = 0 as the reference, :290), so
-        // p <= 2^kLazyRebase and the O / l rescale of the reference's every-tile alpha (:187-199) is needed
-        // only then -- at C3 on no tile after the first (against 49 % of tiles with the exact running max).
-        // The result differs from the reference's only in the rounding of half(p) (p scaled by 2^delta,
-        // delta < kLazyRebase, not a power of two): <= 1.2e-4 at N = 32, 1e-5 at N = 4096 (within 2e-4).
-        const float xm = mx * c_log2;
-        if (__builtin_amdgcn_ballot_w64(xm > m_run + kLazyRebase)) {
-            const float m_b = xm > m_run + kLazyRebase ? xm : m_run;  // per row; 1 for the others
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_run));
+        float ts = tree_sum16(p);  // this lane's half of the keys; the halves are joined once, in the epilogue
+        const uint64_t over = __builtin_amdgcn_ballot_w64(ts > kLazySumCap);
+        if (over) {  // rare (wave-uniform): rebase the rows with a half above the cap, recompute the tile
+            float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);  // max3 chain
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[r]), s[r + 1]);
+            mx = half_swap_max(fmaxf(mx, s[15]));
+            const uint32_t rows = (uint32_t)over | (uint32_t)(over >> 32);
+            const float m_b = ((rows >> col) & 1u) ? mx * c_log2 : m_run;  // per row; alpha 1 for the others
             const float alpha = __builtin_amdgcn_exp2f(m_run - m_b);
             l_run *= alpha;
 #pragma unroll
             for (int m = 0; m < MB; ++m) o[m] *= alpha;
             m_run = m_b;
-        }
-        float p[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_run));
+            for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c_log2, -m_run));
+            ts = tree_sum16(p);
+        }
         v8h pop[2];
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
@@ -178,8 +184,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & F16_LB4) ? 4 : ((FL & F16_LB1) ? 
             pop[r >> 3][r & 7] = h2[0];
             pop[r >> 3][(r & 7) + 1] = h2[1];
         }
-        // this lane's half of the keys; the halves are joined once, in the epilogue
-        l_run += tree_sum16(p);  // :198 (alpha folded into the rebase above)
+        l_run += ts;  // :198 (alpha folded into the rebase above)
 #pragma unroll
         for (int m = 0; m < MB; ++m) {
             const int d = 32 * m + col;

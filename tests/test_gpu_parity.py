@@ -735,11 +735,12 @@ def test_fp16_lazy_base_contract(dev, oracle_mod, N, d, dist):
 @pytest.mark.parametrize("variant,T", [("fa_tc_int8_pt", 4.0), ("fa_tc_v1a", 8.0)])
 @pytest.mark.parametrize("d", [32, 64, 128])
 def test_lazy_base_staircase(dev, oracle_mod, variant, T, d):
-    """The lazy softmax base at its limit (r06): every 32-key tile's row maxima sit
-    0.95 T log2 units above the previous tile's (T = 4 per-tensor, 8 fp16), so the base lags by up to
-    0.95 T on every other tile and moves on the next -- the per-tensor Pi reach ~2^3.8 * 127 = 1773 of the
-    2047 an f16 subnormal holds, the fp16 P ~2^7.6.  Checked against the kernel's own contract (the
-    per-tensor oracle is lazy; oracle fa_fp16_lazy) and, for fp16, against the reference's algorithm."""
+    """The lazy softmax base near its limit (r06): every 32-key tile's scores sit
+    0.95 T log2 units above the previous tile's, nearly equal within a tile, so the base lags by 0.95 T
+    on every other tile and moves on the next.  Per-tensor (T = 4): the Pi reach ~2^3.8 * 127 = 1773 of the
+    2047 an f16 subnormal holds.  fp16 (T = 8): P ~2^7.6, a key half sums ~3100 of the 4096 cap that moves
+    the base.  Checked against the kernel's own contract (the per-tensor oracle is lazy; oracle
+    fa_fp16_lazy) and, for fp16, against the reference's algorithm."""
     B, N, h = 2, 512, 2
     dm = h * d
     rng = np.random.default_rng(int(T) * 1000 + d)
