@@ -427,9 +427,11 @@ void oracle_fa_int8(const float *Q, const float *K, const float *V, float *out,
  * constant the kernel uses (r06; this mode has no reference numerics to follow):
  *   c = RN22(sQ * RN(RN(1/sqrt(d)) * log2 e) * sK)   (float products; RN22: 22 significant bits)
  *   x = RN(S * c - m)   (S the int32 Q.K, one rounding: the kernel's fused multiply-add),
- *   row max xm = RN(S_max * c); lazy base m: moves to xm only when xm > m + 4 (m0 = 0),
- *   p = 2^x in [0, 16],  Pi = min(rint(127 p), 2047),  alpha = 2^(m_old - m_new),
- *   l = alpha l + sum(p),  O = alpha O + (float)(Pi.Vi)[int32],
+ *   row max xm = RN(S_max * c); lazy base m: max(0, xm) on tile 0 (m0 = 0, the exact rule); on a later
+ *   tile it moves to xm only when the p of one of the row's two key halves (keys j with bit 2 of j clear /
+ *   set: the kernel's lane halves, summed in its order) sum above 2047/127 -- then the tile's p are
+ *   recomputed -- so p <= 2047/127,  Pi = min(rint(127 p), 2047),  alpha = 2^(m_old - m_new),
+ *   l = alpha l + sum(p) (per key half, joined at the end),  O = alpha O + (float)(Pi.Vi)[int32],
  *   out = l > 1e-20 ? (O * (sV / 127)) / l : 0.                                   */
 /* ------------------------------------------------------------------------- */
 typedef struct {
@@ -452,7 +454,12 @@ void oracle_quantize_heads_pt(const float *X, int B, int N, int d_model, int h, 
     parallel_for((long)B * h, 0, quantize_tensor_item, &c);
 }
 
-#define PT_REBASE_LOG2 4.0f /* the kernel's kPtRebase */
+static float tree_sum16_of(const float *p) { /* the kernel's tree_sum16 order */
+    float a = (p[0] + p[1]) + (p[2] + p[3]), b = (p[4] + p[5]) + (p[6] + p[7]);
+    float c = (p[8] + p[9]) + (p[10] + p[11]), d = (p[12] + p[13]) + (p[14] + p[15]);
+    return (a + b) + (c + d);
+}
+#define PT_SUM_CAP (2047.0f / 127.0f) /* the kernel's kPtSumCap */
 /* the kernel's score constant (qmha_fa_int8.hip: c_log2 on the host, cq, c_pt) */
 static float pt_score_constant(float sQ, float sK, int dh) {
     const float c_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
@@ -476,9 +483,9 @@ static void fa_int8_pt_item(long item, void *vctx) {
     const float cc = pt_score_constant(c->sQ[bh], c->sK[bh], dh);
 
     float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
-    float l[GROUP], m_prev[GROUP];
+    float l[GROUP][2], m_prev[GROUP];
     for (int r = 0; r < GROUP; ++r) {
-        l[r] = 0.0f;
+        l[r][0] = l[r][1] = 0.0f;
         m_prev[r] = 0.0f; /* m0 = 0, as fa_tc_int8_b.cu:402 */
     }
     int32_t S[GROUP][GROUP];
@@ -492,20 +499,28 @@ static void fa_int8_pt_item(long item, void *vctx) {
                 S[r][j] = acc;
             }
         for (int r = 0; r < GROUP; ++r) {
-            /* lazy base (r06): the row's base moves to the tile's row max only when that max passes it by
-             * more than 4 log2 units, so p <= 16 and Pi <= 2032 */
+            /* lazy base (r06): tile 0 takes max(m0, row max); later tiles move the base to the row max only
+             * when one of the row's key halves sums above the cap, so p <= 2047/127 and Pi <= 2047 */
             int32_t smax = S[r][0];
             for (int j = 1; j < GROUP; ++j) smax = S[r][j] > smax ? S[r][j] : smax;
             const float xm = (float)smax * cc;
-            const float m_new = xm > m_prev[r] + PT_REBASE_LOG2 ? xm : m_prev[r];
-            float p[GROUP];
-            for (int j = 0; j < GROUP; ++j) /* S * cc is exact in double (< 53 bits): one rounding */
-                p[j] = exp2f((float)((double)S[r][j] * (double)cc - (double)m_new));
-            float sum_new = xor_tree_sum32(p);
-            float alpha = exp2f(m_prev[r] - m_new);
-            l[r] = fmaf(alpha, l[r], sum_new);
+            float alpha = 1.0f;
+            if (t == 0) m_prev[r] = fmaxf(m_prev[r], xm);
+            float p[GROUP], ts[2];
+            for (int pass = 0; pass < 2; ++pass) {
+                for (int j = 0; j < GROUP; ++j) /* S * cc is exact in double (< 53 bits): one rounding */
+                    p[j] = exp2f((float)((double)S[r][j] * (double)cc - (double)m_prev[r]));
+                for (int hh = 0; hh < 2; ++hh) { /* lane half hh holds keys (i & 3) + 8 (i >> 2) + 4 hh */
+                    float p16[16];
+                    for (int i = 0; i < 16; ++i) p16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
+                    ts[hh] = tree_sum16_of(p16);
+                }
+                if (pass == 1 || t == 0 || !(ts[0] > PT_SUM_CAP || ts[1] > PT_SUM_CAP)) break;
+                alpha = exp2f(m_prev[r] - xm);
+                m_prev[r] = xm;
+            }
+            for (int hh = 0; hh < 2; ++hh) l[r][hh] = fmaf(alpha, l[r][hh], ts[hh]);
             for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
-            m_prev[r] = m_new;
             int Pi[GROUP];
             for (int j = 0; j < GROUP; ++j) {
                 float rr = rintf(p[j] * 127.0f); /* static P scale 1/127; p in [0, 16] */
@@ -522,7 +537,7 @@ static void fa_int8_pt_item(long item, void *vctx) {
     float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * c->d_model + head * dh;
     for (int r = 0; r < GROUP; ++r)
         for (int d = 0; d < dh; ++d)
-            out[(size_t)r * c->d_model + d] = (l[r] > 1e-20f) ? (O[r * dh + d] * sVq) / l[r] : 0.0f;
+            out[(size_t)r * c->d_model + d] = (l[r][0] + l[r][1] > 1e-20f) ? (O[r * dh + d] * sVq) / (l[r][0] + l[r][1]) : 0.0f;
     free(O);
 }
 
@@ -636,11 +651,6 @@ void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,
  * kernel's order (16-key trees, halves joined at the end).  The reference (oracle_fa_fp16 above) moves m
  * on every tile; the two differ only in the rounding of half(p).  Used by the tests to pin the kernel
  * tightly (the reference bound is checked against oracle_fa_fp16). */
-static float tree_sum16_of(const float *p) { /* the kernel's tree_sum16 order */
-    float a = (p[0] + p[1]) + (p[2] + p[3]), b = (p[4] + p[5]) + (p[6] + p[7]);
-    float c = (p[8] + p[9]) + (p[10] + p[11]), d = (p[12] + p[13]) + (p[14] + p[15]);
-    return (a + b) + (c + d);
-}
 static void fa_fp16_lazy_item(long item, void *vctx) {
     fa_ctx *c = (fa_ctx *)vctx;
     int N = c->N, dm = c->d_model, dh = dm / c->h, G = N / GROUP;

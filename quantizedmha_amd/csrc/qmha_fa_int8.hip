@@ -43,9 +43,10 @@ namespace qmha {
 
 // log2(e): the softmax runs in base 2 (v_exp_f32), scores pre-multiplied by log2(e).
 static constexpr float kLog2e = 1.4426950408889634f;
-// The per-tensor mode's lazy softmax base: p <= 2^4, so Pi = rint(127 p f) <= 2032 stays
-// below 2048, where the magic-number Pi bits are still the f16 encoding of Pi * 2^-24.
-static constexpr float kPtRebase = 4.0f;
+// The per-tensor mode's lazy softmax base: a row's base moves only when the p of one of its
+// key halves sum above 2047/127 on a tile, so every p <= 2047/127 and Pi = rint(127 p) <= 2047 stays below
+// 2048, where the magic-number Pi bits are still the f16 encoding of Pi * 2^-24.
+static constexpr float kPtSumCap = 2047.0f / 127.0f;
 
 // A NaN in the caller's Q becomes 0 before the quantiser sees it, explicitly (integer test on the
 // bits): the reference's fmaxf drops a NaN from the group absmax and __float2int_rn maps it to 0
@@ -525,21 +526,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         if constexpr (!PT) c = __int_as_float((__float_as_int(c) + 2) & ~3);
         const float sfmax = __int_as_float(mxi) - QMHA_MAGIC_RNE;  // exact float(S_max)
         const float xm = sfmax * c;
-        if constexpr (PT)  // lazy base (r06): moves only when the row max passes it by > kPtRebase
-            h_m = xm > m_run + kPtRebase ? xm : m_run;
-        else
-            h_m = fmaxf(m_run, xm);
+        h_m = fmaxf(m_run, xm);
         h_k = fmaf(c, QMHA_MAGIC_RNE, h_m);
         const float delta = fmaf(c, -QMHA_MAGIC_RNE, h_k) - h_m;  // m_eff - m, exact
         h_f = fmaf(delta, 0.69314718055994531f, 1.0f);
         const float xmax = fmaf(sfmax, c, -h_m);
         h_c = c;
-        if constexpr (PT) {  // alpha = 2^(m - m_new); Pi = rint(p * 127) (static P scale), f folded in
-            (void)xmax;
-            h_alpha = __builtin_amdgcn_exp2f(m_run - h_m);
-            h_invp = 127.0f * h_f;
-            return;
-        }
         const float pmax = half_max32_nonneg(__builtin_amdgcn_exp2f(xmax));
         // sP = max(pmax / 127, 1e-8) as pm / 127 with pm = max(pmax, 127e-8), and 1/sP by one
         // v_rcp: within ~2 ulp of the reference's rounded 1/sP, which moves a Pi only when p/sP
@@ -551,6 +543,21 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         h_sp = sp * 16777216.0f;
     };
 
+    // PT lazy base (r06): the base's constants -- Kn, the KFOLD row factor f, 127 f
+    // (Pi = rint(p' 127 f), static P scale) -- change only when the base does, so they are carried across
+    // tiles; the row max is computed on tile 0 (base = max(m0 = 0, row max), the exact rule) and on the
+    // tiles whose key halves sum above kPtSumCap only
+    auto pt_base = [&](float mb) {
+        h_m = mb;
+        h_k = fmaf(c_pt, QMHA_MAGIC_RNE, mb);
+        const float delta = fmaf(c_pt, -QMHA_MAGIC_RNE, h_k) - mb;  // m_eff - m, exact
+        h_f = fmaf(delta, 0.69314718055994531f, 1.0f);
+        h_invp = 127.0f * h_f;
+    };
+    auto pt_rowmax = [&](const v16i& s) {  // RN(S_max * c), log2 units
+        return (__int_as_float(half_swap_max_i(tree_max16_i(s))) - QMHA_MAGIC_RNE) * c_pt;
+    };
+    if constexpr (PT) pt_base(0.0f);
     issue(0);
     if (nst > 1) issue(1);
     qmha_dma_barrier();
@@ -799,9 +806,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         rd_slot(0);
         rd_slot(1);
         QMHA_FENCE();
-        // ---- R0: the tile head (quarter-rate / transcendental), then O *= alpha of tile t-1
-        head(s_cur, t);
-        const float c = h_c, kn = h_k;
+        // ---- R0: tile 0 sets the base (max(m0, row max)); then O *= alpha of tile t-1
+        if constexpr (!has_prev) {
+            pt_base(fmaxf(m_run, pt_rowmax(s_cur)));
+            m_run = h_m;
+        }
+        const float c = c_pt, kn = h_k;
         QMHA_FENCE();
         if constexpr (has_prev) {
             if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
@@ -864,14 +874,32 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- R5
         perms(6, 8);
         QMHA_FENCE();
-        l_run = fmaf(h_alpha, l_run, ((rs0 + rs1) + (rs2 + rs3)) * h_f);  // l = alpha l + sum(p)
-        m_run = h_m;
+        float rsf = ((rs0 + rs1) + (rs2 + rs3)) * h_f;  // this lane's key half: sum(p) = sum(p') f
+        float alpha_t = 1.0f;
+        if constexpr (has_prev) {  // (tile 0 set its base to the row max: p <= 1)
+            const uint64_t over = __builtin_amdgcn_ballot_w64(rsf > kPtSumCap);
+            if (over) {  // rare (wave-uniform): rebase the rows with a half above the cap, redo the tile's P
+                const float xm = pt_rowmax(s_cur);
+                const uint32_t rows = (uint32_t)over | (uint32_t)(over >> 32);
+                const float mb = ((rows >> col) & 1u) ? xm : m_run;
+                alpha_t = __builtin_amdgcn_exp2f(m_run - mb);
+                pt_base(mb);
+                m_run = mb;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c_pt, -h_k);
+                exps(0, 16);
+                quant(0, 16);
+                perms(0, 8);
+                rsf = tree_sum16(p) * h_f;
+            }
+        }
+        l_run = fmaf(alpha_t, l_run, rsf);  // l = alpha l + sum(p)
         QMHA_FENCE();
         mf_slot(5);
         QMHA_FENCE();
         pp[0] = pc[0];
         pp[1] = pc[1];
-        alpha_prev = h_alpha;
+        alpha_prev = alpha_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
     auto run_iter = [&](int t, auto HP, auto HN, auto PH) {

@@ -732,38 +732,48 @@ def test_fp16_lazy_base_contract(dev, oracle_mod, N, d, dist):
     assert_parity("fa_tc_v1a", out, oracle_mod.fa_fp16(Q, K, V, h * d, h))
 
 
-@pytest.mark.parametrize("variant,T", [("fa_tc_int8_pt", 4.0), ("fa_tc_v1a", 8.0)])
+@pytest.mark.parametrize("variant,cap", [("fa_tc_int8_pt", 2047.0 / 127.0), ("fa_tc_v1a", 4096.0)])
 @pytest.mark.parametrize("d", [32, 64, 128])
-def test_lazy_base_staircase(dev, oracle_mod, variant, T, d):
-    """The lazy softmax base near its limit (r06): every 32-key tile's scores sit
-    0.95 T log2 units above the previous tile's, nearly equal within a tile, so the base lags by 0.95 T
-    on every other tile and moves on the next.  Per-tensor (T = 4): the Pi reach ~2^3.8 * 127 = 1773 of the
-    2047 an f16 subnormal holds.  fp16 (T = 8): P ~2^7.6, a key half sums ~3100 of the 4096 cap that moves
-    the base.  Checked against the kernel's own contract (the per-tensor oracle is lazy; oracle
-    fa_fp16_lazy) and, for fp16, against the reference's algorithm."""
+def test_lazy_base_staircase(dev, oracle_mod, variant, cap, d):
+    """The lazy softmax base near its cap (r06; a row's base moves only when the p of
+    one of its key halves sum above the cap: 2047/127 per-tensor, 2^12 fp16).  In every 32-key tile two
+    keys -- one per lane half -- score 0.95 log2(cap) log2 units above the previous tile's, the other 30
+    sit 8 units below them, so a half sums just under the cap on every other tile (the per-tensor Pi reach
+    ~1800 of the 2047 an f16 subnormal holds, the fp16 P ~3800) and the base moves on the next.  Checked
+    against the kernel's own contract (the per-tensor oracle is lazy; oracle fa_fp16_lazy) and, for fp16,
+    against the reference's algorithm."""
     B, N, h = 2, 512, 2
     dm = h * d
-    rng = np.random.default_rng(int(T) * 1000 + d)
+    rng = np.random.default_rng(int(cap) + d)
     Q = (0.5 + 0.01 * rng.standard_normal((B, N, dm))).astype(np.float32)
     # log2-unit score of a key at level a: 0.5 * a * d / sqrt(d) * log2(e)
-    step = 0.95 * T / (0.5 * np.sqrt(d) * np.log2(np.e))
-    level = np.repeat(np.arange(N // 32) * step, 32)[None, :, None]
-    K = (level + 0.01 * rng.standard_normal((B, N, dm))).astype(np.float32)
+    unit = 1.0 / (0.5 * np.sqrt(d) * np.log2(np.e))
+    hi = np.arange(N // 32) * 0.95 * np.log2(cap) * unit
+    level = np.repeat(hi, 32) - 8.0 * unit
+    level[0::32] = hi  # key 0 of each tile (lane half 0) and key 4 (half 1) lead their tile
+    level[4::32] = hi
+    K = (level[None, :, None] + 0.01 * rng.standard_normal((B, N, dm))).astype(np.float32)
     V = rng.standard_normal((B, N, dm)).astype(np.float32)
     out = run(variant, Q, K, V, dm, h, dev)
     if variant == "fa_tc_int8_pt":
         assert_parity(variant, out, oracle_mod.fa_int8_pt(Q, K, V, dm, h))
         return
-    # scores up to ~120 log2 units: the MFMA's fp32 summation order moves a score by ~1e-4 log2 units
-    # against the oracle's sequential sum, which flips half(p) roundings (observed 1.2-1.4e-4), so the
-    # lazy contract is held to the fp16 oracle bound here, not to FP16_LAZY_TOL
+    # Two dominant keys per row with p ~ 2^11.4 (the reference's dominant p is 1, exact in half): a ~1e-5
+    # log2-unit score difference from the MFMA's fp32 summation order flips half(p) of a dominant key
+    # (one half ulp: at most 2^-10 relative) and moves the row by up to 2^-10 max|V| (observed 1.4e-3 against
+    # fa_fp16_lazy, with max|V| = 4.4).  So
+    # the criteria here: as accurate as the reference's algorithm against exact attention, and within that
+    # flip bound of the kernel's own contract
+    exact = oracle_mod.cpu_attention(Q, K, V, dm, h)
+    e_gpu = float(np.abs(out.astype(np.float64) - exact).max())
+    e_ref = float(np.abs(oracle_mod.fa_fp16(Q, K, V, dm, h).astype(np.float64) - exact).max())
+    parity_log.record(f"test_lazy_base_staircase[{variant}-{d}]", "fa_tc_v1a (vs fp32 attn)", e_gpu, 0.0, 1.1 * e_ref)
+    assert e_gpu <= 1.1 * e_ref, (e_gpu, e_ref)
     lazy = oracle_mod.fa_fp16_lazy(Q, K, V, dm, h)
     err = float(np.abs(out.astype(np.float64) - lazy).max())
-    tol = TOL_ORACLE["fa_tc_v1a"]
+    tol = 2.0 ** -10 * float(np.abs(V).max())
     parity_log.record(f"test_lazy_base_staircase[{variant}-{d}]", "fa_tc_v1a (vs lazy)", err, 0.0, tol)
-    assert err <= tol, err
-    # few dominant keys per row: one exp2-vs-expf ulp flips half(p), as in test_growing_scores_reanchor
-    assert_parity(variant, out, oracle_mod.fa_fp16(Q, K, V, dm, h), scale=5.0)
+    assert err <= tol, (err, tol)
 
 
 def test_c3_fp16_full_config_all_heads(dev, oracle_mod):

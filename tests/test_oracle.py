@@ -209,6 +209,15 @@ def _pt_score_constant(sQ, sK, d):
     return ((c + np.uint32(2)) & np.uint32(0xFFFFFFFC)).view(np.float32)[0]
 
 
+def _tree_sum16_rows(p):
+    """The kernels' tree_sum16 order over the 16 columns of p (float32)."""
+    a = (p[:, 0] + p[:, 1]) + (p[:, 2] + p[:, 3])
+    b = (p[:, 4] + p[:, 5]) + (p[:, 6] + p[:, 7])
+    c = (p[:, 8] + p[:, 9]) + (p[:, 10] + p[:, 11])
+    d = (p[:, 12] + p[:, 13]) + (p[:, 14] + p[:, 15])
+    return (a + b) + (c + d)
+
+
 def _np_fa_int8_pt(Q, K, V, h):
     """numpy restatement of oracle_fa_int8_pt for one sequence (base 2, the kernel's score constant;
     float32 arithmetic except x = S * c - m, rounded once from float64 like the kernel's fma)."""
@@ -224,23 +233,36 @@ def _np_fa_int8_pt(Q, K, V, h):
             qs.append((np.clip(np.rint(X[:, sl] * (f(1.0) / s)), -128, 127).astype(np.int64), s))
         (Qi, sQ), (Ki, sK), (Vi, sV) = qs
         c = _pt_score_constant(sQ, sK, d)
+        halves = [np.array([(i & 3) + 8 * (i >> 2) + 4 * hh for i in range(16)]) for hh in range(2)]
+        cap = f(2047.0) / f(127.0)
         for g in range(N // 32):
             rows = slice(32 * g, 32 * g + 32)
             O = np.zeros((32, d), f)
-            l = np.zeros(32, f)
+            l = np.zeros((32, 2), f)
             m = np.zeros(32, f)
             for t in range(N // 32):
                 cols = slice(32 * t, 32 * t + 32)
                 S = Qi[rows] @ Ki[cols].T
-                xm = S.max(axis=1).astype(f) * c  # lazy base (r06): moves only past base + 4
-                m_new = np.where(xm > m + f(4.0), xm, m).astype(f)
-                x = (S.astype(np.float64) * np.float64(c) - m_new[:, None].astype(np.float64)).astype(f)
-                p = np.exp2(x).astype(f)
-                alpha = np.exp2(m - m_new).astype(f)
-                l = alpha * l + p.sum(axis=1, dtype=f)
+                xm = S.max(axis=1).astype(f) * c
+                if t == 0:  # lazy base (r06): tile 0 takes max(m0, row max) ...
+                    m = np.maximum(m, xm).astype(f)
+
+                def tile_p(base):
+                    x = (S.astype(np.float64) * np.float64(c) - base[:, None].astype(np.float64)).astype(f)
+                    p = np.exp2(x).astype(f)
+                    return p, np.stack([_tree_sum16_rows(p[:, hv]) for hv in halves], axis=1)
+                p, ts = tile_p(m)
+                alpha = np.ones(32, f)
+                if t > 0:  # ... later tiles move it to the row max when a key half sums above the cap
+                    rb = (ts > cap).any(axis=1)
+                    alpha = np.where(rb, np.exp2(m - xm), f(1.0)).astype(f)
+                    m = np.where(rb, xm, m).astype(f)
+                    p2, ts2 = tile_p(m)
+                    p, ts = np.where(rb[:, None], p2, p), np.where(rb[:, None], ts2, ts)
+                l = (alpha[:, None] * l + ts).astype(f)
                 Pi = np.minimum(np.rint(p * f(127.0)), 2047).astype(np.int64)
                 O = O * alpha[:, None] + (Pi @ Vi[cols]).astype(f)
-                m = m_new
+            l = l[:, 0] + l[:, 1]
             out[rows, sl] = np.where(l[:, None] > 1e-20, O * (sV / f(127.0)) / l[:, None], 0)
     return out
 
