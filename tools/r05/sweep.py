@@ -2,7 +2,7 @@
 """Extended parity sweep on the GPU (evidence beyond the pytest suite, not part of it): random shapes
 (B 1..6, N = 32 * (1..96), H 1..8, d in {32, 64, 128}, N(0, 0.5^2) or U[0, 1) inputs) through every
 fused-attention variant against the oracle, at the suite's criteria (tests/test_gpu_parity.py
-assert_parity), fa_tc_v1a also against its lazy-base contract (oracle fa_fp16_lazy, FP16_LAZY_TOL).  (Until r05 it also compared the one-launch opt-ins, removed in r06.)  Test infrastructure: the oracle is the checker.
+assert_parity), fa_tc_v1a also against its lazy-base contract (oracle fa_fp16_lazy, fp16_lazy_tol).  (Until r05 it also compared the one-launch opt-ins, removed in r06.)  Test infrastructure: the oracle is the checker.
     python tools/r05/sweep.py [--n 200] [--seed 5] [--variants fa_tc_int8_pt]"""
 import argparse
 import os
@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from oracle import oracle as oracle_mod  # noqa: E402
 from quantizedmha_amd import _lib, torch_ext  # noqa: E402
-from tests.test_gpu_parity import FP16_LAZY_TOL, INT8_TOL_TIGHT, INT8_FLIP_FRAC, INT8_FLIP_FRAC_PT, TOL_ORACLE, int8_tol  # noqa: E402
+from tests.test_gpu_parity import INT8_TOL_TIGHT, INT8_FLIP_FRAC, INT8_FLIP_FRAC_PT, TOL_ORACLE, fp16_lazy_tol, int8_tol  # noqa: E402
 
 VARIANTS = ("fa_tc_int8_b", "fa_tc_int8_pt", "fa_tc_v1a", "fa")
 
@@ -80,7 +80,7 @@ def main():
             if v == "fa_tc_v1a":  # since r06 also against the kernel's own lazy-base contract (oracle fa_fp16_lazy)
                 el = float(np.abs(out.cpu().numpy().astype(np.float64) - oracle_mod.fa_fp16_lazy(Q, K, V, dm, H, nthreads=16)).max())
                 worst["fa_tc_v1a (vs lazy)"] = max(worst.get("fa_tc_v1a (vs lazy)", 0.0), el)
-                ok = ok and el <= FP16_LAZY_TOL
+                ok = ok and el <= fp16_lazy_tol(N)
                 line.append(f"[lazy {el:.2e}]")
             fails += not ok
             line.append(f"{v} {e:.2e}/{frac:.1e}{'' if ok else ' FAIL'}")
