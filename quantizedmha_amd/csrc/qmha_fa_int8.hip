@@ -517,7 +517,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     static_assert(KFOLD, "the pipelined kernel ships with FL_MAGIC | FL_KFOLD");
     // per-tile head results: score scale c', running max m, Kn, row factor f, sP (with the 2^24 of
     // the f16-subnormal P entries), 1/sP (with f), alpha (PT)
-    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f;
+    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f, h_cap = 0.0f;
     // PT: the score scale sQ * sK * log2(e) / sqrt(d) is one constant per head (KFOLD-rounded once)
     const float c_pt = PT ? __int_as_float((__float_as_int(cq * skb[0]) + 2) & ~3) : 0.0f;
     auto head = [&](const v16i& s, int t) {
@@ -553,6 +553,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float delta = fmaf(c_pt, -QMHA_MAGIC_RNE, h_k) - mb;  // m_eff - m, exact
         h_f = fmaf(delta, 0.69314718055994531f, 1.0f);
         h_invp = 127.0f * h_f;
+        h_cap = kPtSumCap / h_f;  // the cap on sum(p') = sum(p) / f
     };
     auto pt_rowmax = [&](const v16i& s) {  // RN(S_max * c), log2 units
         return (__int_as_float(half_swap_max_i(tree_max16_i(s))) - QMHA_MAGIC_RNE) * c_pt;
@@ -730,6 +731,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     // into O; O takes tile t-1's alpha at the start of iteration t (before P@V of t-1 lands, after
     // P@V of t-2 has), so no MFMA result is waited on.
     float alpha_prev = 1.0f;  // the alpha of the tile whose P@V this iteration adds
+    bool rescale_prev = false;  // wave-uniform: that tile rebased some row (alpha_prev != 1 somewhere)
     auto iter_pt = [&](int t, auto HP, auto HN, auto PH) {
         constexpr bool has_prev = decltype(HP)::value, has_next = decltype(HN)::value;
         constexpr int ph = decltype(PH)::value;
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         const float c = c_pt, kn = h_k;
         QMHA_FENCE();
         if constexpr (has_prev) {
-            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {
+            if (rescale_prev) {
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
             }
@@ -874,15 +876,18 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- R5
         perms(6, 8);
         QMHA_FENCE();
-        float rsf = ((rs0 + rs1) + (rs2 + rs3)) * h_f;  // this lane's key half: sum(p) = sum(p') f
+        float ts = (rs0 + rs1) + (rs2 + rs3);  // this lane's key half: sum(p') (sum(p) = sum(p') f)
         float alpha_t = 1.0f;
+        bool rescale_t = false;
         if constexpr (has_prev) {  // (tile 0 set its base to the row max: p <= 1)
-            const uint64_t over = __builtin_amdgcn_ballot_w64(rsf > kPtSumCap);
+            const uint64_t over = __builtin_amdgcn_ballot_w64(ts > h_cap);
             if (over) {  // rare (wave-uniform): rebase the rows with a half above the cap, redo the tile's P
+                rescale_t = true;
                 const float xm = pt_rowmax(s_cur);
                 const uint32_t rows = (uint32_t)over | (uint32_t)(over >> 32);
                 const float mb = ((rows >> col) & 1u) ? xm : m_run;
                 alpha_t = __builtin_amdgcn_exp2f(m_run - mb);
+                l_run *= alpha_t;
                 pt_base(mb);
                 m_run = mb;
 #pragma unroll
@@ -890,16 +895,17 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                 exps(0, 16);
                 quant(0, 16);
                 perms(0, 8);
-                rsf = tree_sum16(p) * h_f;
+                ts = tree_sum16(p);
             }
         }
-        l_run = fmaf(alpha_t, l_run, rsf);  // l = alpha l + sum(p)
+        l_run = fmaf(ts, h_f, l_run);  // l = alpha l + sum(p)
         QMHA_FENCE();
         mf_slot(5);
         QMHA_FENCE();
         pp[0] = pc[0];
         pp[1] = pc[1];
         alpha_prev = alpha_t;
+        rescale_prev = rescale_t;
         if constexpr (has_next) s_cur = s_nxt;
     };
     auto run_iter = [&](int t, auto HP, auto HN, auto PH) {
@@ -953,7 +959,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     {
         const int t = G - 1;
         if constexpr (PT) {
-            if (__builtin_amdgcn_ballot_w64(alpha_prev != 1.0f)) {  // O still owes the last tile's alpha
+            if (rescale_prev) {  // O still owes the last tile's alpha
 #pragma unroll
                 for (int m = 0; m < MB; ++m) o[m] *= alpha_prev;
             }
