@@ -78,7 +78,7 @@ def header_deps():
 # v_max (x, x) in front of it (5 per fp16 tile); the main kernels only.  The pre-passes that read the
 # caller's Q/K/V (qmha_prepass.hip) keep default IEEE semantics (round-2 ADVICE)
 FILE_FLAGS = {"qmha_fa_int8.hip": ["-fno-slp-vectorize", "-fno-honor-nans"] + os.environ.get("QMHA_INT8_FLAGS", "").split(),
-              "qmha_fa_f16.hip": ["-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split(),
+              "qmha_fa_f16.hip": ["-fno-slp-vectorize", "-fno-honor-nans"] + os.environ.get("QMHA_F16_FLAGS", "").split(),
               "qmha_fa_f32.hip": os.environ.get("QMHA_F32_FLAGS", "").split()}
 
 
