@@ -516,8 +516,8 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
     constexpr bool KFOLD = MAGIC && (FL & FL_KFOLD);
     static_assert(KFOLD, "the pipelined kernel ships with FL_MAGIC | FL_KFOLD");
     // per-tile head results: score scale c', running max m, Kn, row factor f, sP (with the 2^24 of
-    // the f16-subnormal P entries), 1/sP (with f), alpha (PT)
-    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_alpha = 1.0f, h_cap = 0.0f;
+    // the f16-subnormal P entries), 1/sP (with f); PT: 127 f and the sum cap / f (carried across tiles)
+    float h_c = 0.0f, h_m = 0.0f, h_k = 0.0f, h_f = 1.0f, h_sp = 0.0f, h_invp = 0.0f, h_cap = 0.0f;
     // PT: the score scale sQ * sK * log2(e) / sqrt(d) is one constant per head (KFOLD-rounded once)
     const float c_pt = PT ? __int_as_float((__float_as_int(cq * skb[0]) + 2) & ~3) : 0.0f;
     auto head = [&](const v16i& s, int t) {
@@ -620,15 +620,9 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
                         if (has_next) qk(JIT ? kop(ks) : kk[ks], ks);
                     } else {
                         const int m = op >> 1, ks = op & 1;
-                        if (has_prev) {
-                            if constexpr (PT) {  // P@V straight into O
-                                o[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks], o[m], 0,
-                                                                              0, 0);
-                            } else {
-                                a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
-                                                                              ks == 0 ? v16f{} : a[m], 0, 0, 0);
-                            }
-                        }
+                        if (has_prev)
+                            a[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(JIT ? vop(m, ks) : vv[m][ks], pp[ks],
+                                                                          ks == 0 ? v16f{} : a[m], 0, 0, 0);
                     }
                 }
             }
@@ -640,7 +634,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // re-anchor (rare) before this tile's shift 2^(m_new - anchor) is formed, so it stays <= 2^48
         // however far the running max jumps (a first tile ~100 log2 units above m0 = 0 would
         // overflow it); the pending tile t-1 carries its factor in scale_prev
-        if (!PT && __builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
+        if (__builtin_amdgcn_ballot_w64(m_new - anchor > 48.0f)) {
             const float f = __builtin_amdgcn_exp2f(anchor - m_new);
 #pragma unroll
             for (int m = 0; m < MB; ++m) o[m] *= f;
@@ -652,7 +646,7 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         QMHA_FENCE();
         // ---- B: P scale, scores of rows 0..7
         const float sp = h_sp, invp = h_invp;
-        const float e = PT ? 1.0f : __builtin_amdgcn_exp2f(m_new - anchor);
+        const float e = __builtin_amdgcn_exp2f(m_new - anchor);
         float x[16];
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = fmaf(__int_as_float(s_cur[r]), c, -kn);
@@ -696,21 +690,12 @@ __global__ __launch_bounds__(WAVES * 64, (FL & FL_LB2) ? 2 : ((FL & FL_LB4) ? 4 
         // ---- G: row sum (unquantised p, :336), anchored l, this tile's O scale
         // this lane's 16 keys only: the two halves of l are joined once, in the epilogue
         const float rs = tree_sum16(p);
-        if constexpr (PT)
-            l_run = fmaf(h_alpha, l_run, rs * h_f);  // l = alpha * l + sum(p)
-        else
-            l_run = fmaf(rs, e * h_f, l_run);
+        l_run = fmaf(rs, e * h_f, l_run);
         m_run = m_new;
         // sp carries 2^24 (P entries are Pi * 2^-24)
-        const float scale_t = PT ? 0.0f : sp * svb[t] * e;
-        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor)); PT: O already
-        // holds tile t-1's P@V, and takes this tile's alpha before tile t's P@V lands next iteration
-        if constexpr (PT) {
-            if (__builtin_amdgcn_ballot_w64(h_alpha != 1.0f)) {
-#pragma unroll
-                for (int m = 0; m < MB; ++m) o[m] *= h_alpha;
-            }
-        } else if constexpr (has_prev) {
+        const float scale_t = sp * svb[t] * e;
+        // ---- H: fold the pending tile's P@V into O (o += T * sP * sV * 2^(m - anchor))
+        if constexpr (has_prev) {
 #pragma unroll
             for (int m = 0; m < MB; ++m)
 #pragma unroll
