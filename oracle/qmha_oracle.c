@@ -645,10 +645,11 @@ void oracle_fa_fp16(const float *Q, const float *K, const float *V, float *out,
 
 /* The fp16 GPU kernel's own contract (r06): fa_tc_v1a's arithmetic with the softmax in
  * base 2 (x = S * (1/sqrtf(d)) * log2 e, exp2) and a LAZY base: p = exp2(x - m) against a per-row base m
- * (m0 = 0) that moves to the tile's row max only when the p of one of the row's two key halves (the
- * kernel's lane halves: keys j with bit 2 of j clear / set) sum above 2^12 on that tile; then O and l are
- * scaled by exp2(m_old - m_new) and the tile's p recomputed.  l is kept per half and summed in the
- * kernel's order (16-key trees, halves joined at the end).  The reference (oracle_fa_fp16 above) moves m
+ * (m0 = 0) that moves to the tile's row max only when the p of one of the row's key parts sum above 2^12
+ * on that tile; then O and l are scaled by exp2(m_old - m_new) and the tile's p recomputed.  The parts
+ * are the kernel's lanes: at d = 64 / 128 (the 16x16x32 kernel) four quarters of eight keys, lane group g
+ * holding keys kap16(j >> 2, 4 g + (j & 3)); at other d (the 32x32x16 kernel) two halves of sixteen, keys
+ * j with bit 2 of j clear / set.  l is kept per part and summed in the kernel's order.  The reference (oracle_fa_fp16 above) moves m
  * on every tile; the two differ only in the rounding of half(p).  Used by the tests to pin the kernel
  * tightly (the reference bound is checked against oracle_fa_fp16). */
 static void fa_fp16_lazy_item(long item, void *vctx) {
@@ -666,9 +667,11 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
     float *kt = (float *)malloc(sizeof(float) * GROUP * dh);
     float *vv = (float *)malloc(sizeof(float) * GROUP * dh);
     float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
-    float l[GROUP][2], m[GROUP], s[GROUP][GROUP], ph[GROUP][GROUP];
+    const int quarters = dh == 64 || dh == 128; /* the 16x16x32 kernel's lane parts */
+    const int nparts = quarters ? 4 : 2;
+    float l[GROUP][4], m[GROUP], s[GROUP][GROUP], ph[GROUP][GROUP];
     for (int r = 0; r < GROUP; ++r) {
-        l[r][0] = l[r][1] = 0.0f;
+        l[r][0] = l[r][1] = l[r][2] = l[r][3] = 0.0f;
         m[r] = 0.0f;
         for (int d = 0; d < dh; ++d)
             q[r * dh + d] = oracle_f16_to_f32(oracle_f32_to_f16(Qb[(size_t)(g * GROUP + r) * dm + d]));
@@ -686,27 +689,36 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
                 s[r][j] = acc; /* raw S: the kernel scales inside the exponent */
             }
         for (int r = 0; r < GROUP; ++r) {
-            float p[GROUP], ts[2];
+            float p[GROUP], ts[4];
             for (int pass = 0; pass < 2; ++pass) {
                 for (int j = 0; j < GROUP; ++j) p[j] = exp2f(fmaf(s[r][j], c_log2, -m[r]));
-                for (int hh = 0; hh < 2; ++hh) { /* lane half hh holds keys (i & 3) + 8 (i >> 2) + 4 hh */
-                    float ph16[16];
-                    for (int i = 0; i < 16; ++i) ph16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
-                    ts[hh] = tree_sum16_of(ph16);
+                int over = 0;
+                for (int hh = 0; hh < nparts; ++hh) {
+                    if (quarters) { /* lane group hh: keys kap16(j >> 2, 4 hh + (j & 3)), summed as a tree */
+                        float q[8];
+                        for (int j = 0; j < 8; ++j) {
+                            const int mm = 4 * hh + (j & 3);
+                            q[j] = p[16 * (mm >> 3) + 4 * ((mm >> 2) & 1) + (mm & 3) + 8 * (j >> 2)];
+                        }
+                        ts[hh] = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                    } else { /* lane half hh: keys (i & 3) + 8 (i >> 2) + 4 hh */
+                        float ph16[16];
+                        for (int i = 0; i < 16; ++i) ph16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
+                        ts[hh] = tree_sum16_of(ph16);
+                    }
+                    over |= ts[hh] > cap;
                 }
-                if (pass == 1 || !(ts[0] > cap || ts[1] > cap)) break;
+                if (pass == 1 || !over) break;
                 float mx = s[r][0]; /* rebase: the row max, O and l scaled, the tile recomputed */
                 for (int j = 1; j < GROUP; ++j) mx = fmaxf(mx, s[r][j]);
                 const float xm = mx * c_log2;
                 const float alpha = exp2f(m[r] - xm);
-                l[r][0] *= alpha;
-                l[r][1] *= alpha;
+                for (int hh = 0; hh < nparts; ++hh) l[r][hh] *= alpha;
                 for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
                 m[r] = xm;
             }
             for (int j = 0; j < GROUP; ++j) ph[r][j] = oracle_f16_to_f32(oracle_f32_to_f16(p[j]));
-            l[r][0] += ts[0];
-            l[r][1] += ts[1];
+            for (int hh = 0; hh < nparts; ++hh) l[r][hh] += ts[hh];
         }
         for (int r = 0; r < GROUP; ++r)
             for (int d = 0; d < dh; ++d) {
@@ -718,7 +730,7 @@ static void fa_fp16_lazy_item(long item, void *vctx) {
     float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * dm + head * dh;
     for (int r = 0; r < GROUP; ++r)
         for (int d = 0; d < dh; ++d) {
-            const float lr = l[r][0] + l[r][1];
+            const float lr = quarters ? (l[r][0] + l[r][1]) + (l[r][2] + l[r][3]) : l[r][0] + l[r][1];
             out[(size_t)r * dm + d] = (lr > 1e-10f) ? O[r * dh + d] / lr : 0.0f;
         }
     free(q);

@@ -136,7 +136,16 @@ void run(const char* name) {
     (void)hipFree(st);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1) {  // r06: the fp16 tile's density after the lazy base (~9 VALU per MFMA)
+        run<0, 6>("32x32x16 f16");
+        run<1, 6>("2x 16x16x32 f16");
+        run<0, 12>("32x32x16 f16");
+        run<1, 12>("2x 16x16x32 f16");
+        run<0, 6>("32x32x16 f16");
+        run<1, 6>("2x 16x16x32 f16");
+        return 0;
+    }
     run<0, 0>("32x32x16 f16");
     run<1, 0>("2x 16x16x32 f16");
     run<0, 12>("32x32x16 f16");
