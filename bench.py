@@ -357,7 +357,7 @@ def isa_ids(variant, d):
     from quantizedmha_amd import isa_id
     pats = {"fa_tc_int8_b": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_quant_int8_kernelILi{d}ELi1E"),
             "fa_tc_int8_pt": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_pt_quant_kernelILi{d}E"),
-            "fa_tc_v1a": (f"qmha_fa_f16_v2_kernelILi{d}E", f"qmha_convert_f16_kernelILi{d}E"),
+            "fa_tc_v1a": (f"qmha_fa_f16_{'v3' if d in (64, 128) else 'v2'}_kernelILi{d}E", f"qmha_convert_f16_kernelILi{d}E"),
             "fa": (f"qmha_fa_f32_v3_kernelILi{d}E", None), "fa_mfma": (f"qmha_fa_f32_mfma_kernelILi{d}E", None),
             "unfused": ("qmha_gemm_f32_mfma_kernel", "qmha_softmax_rows")}.get(variant, (None, None))
     out = {}
