@@ -428,8 +428,8 @@ void oracle_fa_int8(const float *Q, const float *K, const float *V, float *out,
  *   c = RN22(sQ * RN(RN(1/sqrt(d)) * log2 e) * sK)   (float products; RN22: 22 significant bits)
  *   x = RN(S * c - m)   (S the int32 Q.K, one rounding: the kernel's fused multiply-add),
  *   row max xm = RN(S_max * c); lazy base m: max(0, xm) on tile 0 (m0 = 0, the exact rule); on a later
- *   tile it moves to xm only when the p of one of the row's two key halves (keys j with bit 2 of j clear /
- *   set: the kernel's lane halves, summed in its order) sum above 2047/127 -- then the tile's p are
+ *   tile it moves to xm only when the p of one of the row's key parts (the kernel's lanes, summed in its
+ *   order: quarters of eight keys at d = 64, halves of sixteen elsewhere) sum above 2047/127 -- then the tile's p are
  *   recomputed -- so p <= 2047/127,  Pi = min(rint(127 p), 2047),  alpha = 2^(m_old - m_new),
  *   l = alpha l + sum(p) (per key half, joined at the end),  O = alpha O + (float)(Pi.Vi)[int32],
  *   out = l > 1e-20 ? (O * (sV / 127)) / l : 0.                                   */
@@ -483,9 +483,11 @@ static void fa_int8_pt_item(long item, void *vctx) {
     const float cc = pt_score_constant(c->sQ[bh], c->sK[bh], dh);
 
     float *O = (float *)calloc((size_t)GROUP * dh, sizeof(float));
-    float l[GROUP][2], m_prev[GROUP];
+    const int quarters = dh == 64; /* the 16x16 kernel's lane parts (d = 64); halves elsewhere */
+    const int nparts = quarters ? 4 : 2;
+    float l[GROUP][4], m_prev[GROUP];
     for (int r = 0; r < GROUP; ++r) {
-        l[r][0] = l[r][1] = 0.0f;
+        l[r][0] = l[r][1] = l[r][2] = l[r][3] = 0.0f;
         m_prev[r] = 0.0f; /* m0 = 0, as fa_tc_int8_b.cu:402 */
     }
     int32_t S[GROUP][GROUP];
@@ -500,26 +502,38 @@ static void fa_int8_pt_item(long item, void *vctx) {
             }
         for (int r = 0; r < GROUP; ++r) {
             /* lazy base (r06): tile 0 takes max(m0, row max); later tiles move the base to the row max only
-             * when one of the row's key halves sums above the cap, so p <= 2047/127 and Pi <= 2047 */
+             * when one of the row's key parts (the kernel's lanes: quarters at d = 64, halves elsewhere) sums
+             * above the cap, so p <= 2047/127 and Pi <= 2047 */
             int32_t smax = S[r][0];
             for (int j = 1; j < GROUP; ++j) smax = S[r][j] > smax ? S[r][j] : smax;
             const float xm = (float)smax * cc;
             float alpha = 1.0f;
             if (t == 0) m_prev[r] = fmaxf(m_prev[r], xm);
-            float p[GROUP], ts[2];
+            float p[GROUP], ts[4];
             for (int pass = 0; pass < 2; ++pass) {
                 for (int j = 0; j < GROUP; ++j) /* S * cc is exact in double (< 53 bits): one rounding */
                     p[j] = exp2f((float)((double)S[r][j] * (double)cc - (double)m_prev[r]));
-                for (int hh = 0; hh < 2; ++hh) { /* lane half hh holds keys (i & 3) + 8 (i >> 2) + 4 hh */
-                    float p16[16];
-                    for (int i = 0; i < 16; ++i) p16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
-                    ts[hh] = tree_sum16_of(p16);
+                int over = 0;
+                for (int hh = 0; hh < nparts; ++hh) {
+                    if (quarters) { /* lane group hh: keys kap16(j >> 2, 4 hh + (j & 3)), summed as a tree */
+                        float q[8];
+                        for (int j = 0; j < 8; ++j) {
+                            const int mm = 4 * hh + (j & 3);
+                            q[j] = p[16 * (mm >> 3) + 4 * ((mm >> 2) & 1) + (mm & 3) + 8 * (j >> 2)];
+                        }
+                        ts[hh] = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                    } else { /* lane half hh: keys (i & 3) + 8 (i >> 2) + 4 hh */
+                        float p16[16];
+                        for (int i = 0; i < 16; ++i) p16[i] = p[(i & 3) + 8 * (i >> 2) + 4 * hh];
+                        ts[hh] = tree_sum16_of(p16);
+                    }
+                    over |= ts[hh] > PT_SUM_CAP;
                 }
-                if (pass == 1 || t == 0 || !(ts[0] > PT_SUM_CAP || ts[1] > PT_SUM_CAP)) break;
+                if (pass == 1 || t == 0 || !over) break;
                 alpha = exp2f(m_prev[r] - xm);
                 m_prev[r] = xm;
             }
-            for (int hh = 0; hh < 2; ++hh) l[r][hh] = fmaf(alpha, l[r][hh], ts[hh]);
+            for (int hh = 0; hh < nparts; ++hh) l[r][hh] = fmaf(alpha, l[r][hh], ts[hh]);
             for (int d = 0; d < dh; ++d) O[r * dh + d] *= alpha;
             int Pi[GROUP];
             for (int j = 0; j < GROUP; ++j) {
@@ -537,7 +551,10 @@ static void fa_int8_pt_item(long item, void *vctx) {
     float *out = c->out + ((size_t)b * N + (size_t)g * GROUP) * c->d_model + head * dh;
     for (int r = 0; r < GROUP; ++r)
         for (int d = 0; d < dh; ++d)
-            out[(size_t)r * c->d_model + d] = (l[r][0] + l[r][1] > 1e-20f) ? (O[r * dh + d] * sVq) / (l[r][0] + l[r][1]) : 0.0f;
+        {
+            const float lr = quarters ? (l[r][0] + l[r][1]) + (l[r][2] + l[r][3]) : l[r][0] + l[r][1];
+            out[(size_t)r * c->d_model + d] = (lr > 1e-20f) ? (O[r * dh + d] * sVq) / lr : 0.0f;
+        }
     free(O);
 }
 

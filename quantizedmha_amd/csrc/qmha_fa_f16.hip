@@ -542,7 +542,8 @@ static hipError_t fa_f16_d(const F16Workspace& w, const float* Qf, float* O, int
     // Other head sizes (d % 32 == 0, include/config.h:32): 4-wave workgroups, the V operands read at
     // their MFMA, a 2-wave budget at d = 96 and 1 wave above d = 128
     // d = 64 / 128: the 16x16x32 kernel (v3), same box, alternating: C3 -2.5 %, d = 128 -1.9 %; at d = 32 it
-    // measured +2.8 % (93 VGPRs, 5 waves per SIMD against v2's 6), so v2 keeps d = 32 (profiles/r06/ab_f16_mma16/)
+    // measured +2.8 % (93 VGPRs, 5 waves per SIMD against v2's 6; at a 6-wave budget, spilling 11 registers,
+    // +2.9 % / +9 %), so v2 keeps d = 32 (profiles/r06/ab_f16_mma16/)
     if constexpr (D == 64 || D == 128) {
         constexpr int W = D <= 64 ? QMHA_F16_WAVES : 4;
         const int G = N / QMHA_GROUP, nqb = (G + W - 1) / W;

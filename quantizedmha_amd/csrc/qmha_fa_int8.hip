@@ -1084,6 +1084,264 @@ static hipError_t fa_int8_pipe_launch(const Int8Workspace& w, const float* Qf, f
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Per-tensor mode on 16x16 MFMAs (shipped at d = 64): the fp16 v3 kernel's tile
+// (qmha_fa_f16.hip) with the per-tensor contract of the pipe kernel's iter_pt: Q@K^T on
+// v_mfma_i32_16x16x64_i8 from the magic-biased accumulator (KFOLD exponent), P quantised with the static
+// scale into f16-subnormal pairs, P@V on v_mfma_f32_16x16x32_f16 straight into O, the lazy base per query
+// triggered by a lane's key quarter.  Same K rows in the kap16 key order as the fp16 v3 kernel, the V^T
+// slot order unchanged.  No software pipeline: four waves per SIMD interleave instead.
+// ---------------------------------------------------------------------------------------
+__host__ __device__ constexpr int kap16_i8(int kb, int m) { return 16 * (m >> 3) + 4 * ((m >> 2) & 1) + (m & 3) + 8 * kb; }
+
+template <int D, int WAVES, int SG, bool DUMP>
+__global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_int8_pt_v3_kernel(
+    const float* __restrict__ Qf, const int8_t* __restrict__ Ki, const _Float16* __restrict__ Vh,
+    const float* __restrict__ sQt, const float* __restrict__ sK, const float* __restrict__ sV, float* __restrict__ O,
+    int N, int H, int d_model, int nqb, float c_log2, QkDump dbg) {
+    constexpr int KS = D / 64;            // QK k-steps (K = 64)
+    constexpr int DB = D / 16;            // PV d-blocks of 16 rows
+    constexpr int RB = D;                 // K row bytes (int8)
+    constexpr int KBYTES = SG * 32 * RB;  // K per stage
+    constexpr int VBYTES = SG * 32 * D * 2;
+    constexpr int KCH = KBYTES / 16, VCH = VBYTES / 16;
+    static_assert(KCH % 64 == 0 && VCH % 64 == 0 && (KCH / SG) % 64 == 0, "whole KiB LDS-DMA pieces");
+    __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
+
+    const int G = N / QMHA_GROUP;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = wg / nqb, qb0 = wg % nqb;
+    const int b = bh / H, k = bh % H;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int qg = qb0 * WAVES + wave;
+    const bool active = qg < G;
+    const int grp = lane >> 4, r16 = lane & 15;
+
+    // Q quantised with the slice scale into the QK B operand: query 16 qb + r16, d = 64 ks + 16 grp .. +15
+    const float sq = sQt[bh];
+    const float inv_q = 1.0f / sq;
+    v4i qop[2][KS];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (active) {
+                const float* qp = Qf + ((size_t)b * N + (size_t)qg * QMHA_GROUP + 16 * qb + r16) * d_model + (size_t)k * D +
+                                  64 * ks + 16 * grp;
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    const v4f x = *reinterpret_cast<const v4f*>(qp + 4 * c4);
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w |= ((uint32_t)(uint8_t)qmha_quant_i8(nan_to_zero(x[e]), inv_q)) << (8 * e);
+                    qop[qb][ks][c4] = (int)w;
+                }
+            } else {
+                qop[qb][ks] = v4i{0, 0, 0, 0};
+            }
+        }
+    if constexpr (DUMP) {  // the Q operand as held in registers (FL_DUMP twin: qmha_debug_fa_int8_pt_dump)
+        if (active) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    *reinterpret_cast<v4i*>(dbg.Qi + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + 16 * qb + r16) * D + 64 * ks +
+                                            16 * grp) = qop[qb][ks];
+            if (lane == 0) dbg.sQ[(size_t)bh * G + qg] = sq;
+        }
+    }
+    // the score constant sQ * sK * log2(e) / sqrt(d), KFOLD-rounded to 22 bits (as the pipe kernel)
+    const float c_pt = __int_as_float((__float_as_int((sq * c_log2) * sK[bh]) + 2) & ~3);
+    const v4i magic4 = {0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+    v4f o[DB][2];
+#pragma unroll
+    for (int m = 0; m < DB; ++m) o[m][0] = o[m][1] = v4f{};
+    // per query (qb): base m, Kn, the KFOLD row factor f, 127 f, cap / f; l over this lane's keys
+    float m_run[2] = {0.0f, 0.0f}, l_run[2] = {0.0f, 0.0f};
+    float h_k[2], h_f[2], h_invp[2], h_cap[2];
+    auto pt_base = [&](int qb, float mb) {
+        m_run[qb] = mb;
+        h_k[qb] = fmaf(c_pt, QMHA_MAGIC_RNE, mb);
+        const float delta = fmaf(c_pt, -QMHA_MAGIC_RNE, h_k[qb]) - mb;  // m_eff - m, exact
+        h_f[qb] = fmaf(delta, 0.69314718055994531f, 1.0f);
+        h_invp[qb] = 127.0f * h_f[qb];
+        h_cap[qb] = kPtSumCap / h_f[qb];
+    };
+    pt_base(0, 0.0f);
+    pt_base(1, 0.0f);
+
+    const char* kbase = reinterpret_cast<const char*>(Ki + (size_t)bh * N * D);
+    const char* vbase = reinterpret_cast<const char*>(Vh + (size_t)bh * N * D);
+    const int nst = (G + SG - 1) / SG;
+    constexpr int KJ = (KCH / 64 + WAVES - 1) / WAVES, VJ = (VCH / 64 + WAVES - 1) / WAVES;
+    int koff[KJ], voff[VJ];
+#pragma unroll
+    for (int jj = 0; jj < KJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int row = idx / (RB / 16), cc = swz_src<RB>(row, idx % (RB / 16));
+        koff[jj] = row * RB + 16 * cc;
+    }
+#pragma unroll
+    for (int jj = 0; jj < VJ; ++jj) {
+        const int idx = (wave + jj * WAVES) * 64 + lane;
+        const int gq = idx / (4 * D), w = idx % (4 * D);
+        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
+        voff[jj] = gq * 64 * D + d * 64 + 16 * cv;
+    }
+    auto issue = [&](int buf, int st) {
+        const int ngr = min(SG, G - st * SG);
+        char* L = lds[buf];
+#pragma unroll
+        for (int jj = 0; jj < KJ; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < KCH / 64 && inst * 64 < ngr * (KCH / SG))
+                buffer_load_lds16(kbase, N * RB, (lptr_t)(L + inst * 1024), koff[jj], st * KBYTES);
+        }
+#pragma unroll
+        for (int jj = 0; jj < VJ; ++jj) {
+            const int inst = wave + jj * WAVES;
+            if (inst < VCH / 64 && inst * 64 < ngr * (VCH / SG))
+                buffer_load_lds16(vbase, N * D * 2, (lptr_t)(L + KBYTES + inst * 1024), voff[jj], st * VBYTES);
+        }
+    };
+    struct S4 {
+        v4i v[2][2];  // [kb][qb]: magic-biased int32 S^T, rows kap16_i8(kb, 4 grp + i), query 16 qb + r16
+    };
+    auto qk = [&](const char* L, int gi) {
+        S4 s;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const int krow = gi * 32 + kap16_i8(kb, r16);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const v4i kop = *reinterpret_cast<const v4i*>(L + krow * RB + 16 * swz_pos<RB>(krow, 4 * ks + grp));
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+                    s.v[kb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(kop, qop[qb][ks], ks == 0 ? magic4 : s.v[kb][qb], 0, 0, 0);
+            }
+        }
+        return s;
+    };
+    auto rowmax_xm = [&](const S4& s, int qb) {  // RN(S_max * c) of the query's 32 keys (4 lanes x 8)
+        int mx = max(max(max(s.v[0][qb][0], s.v[0][qb][1]), max(s.v[0][qb][2], s.v[0][qb][3])),
+                     max(max(s.v[1][qb][0], s.v[1][qb][1]), max(s.v[1][qb][2], s.v[1][qb][3])));
+        mx = max(mx, __shfl_xor(mx, 16));
+        mx = max(mx, __shfl_xor(mx, 32));
+        return (__int_as_float(mx) - QMHA_MAGIC_RNE) * c_pt;
+    };
+    auto tile = [&](const char* L, int gi, const S4& s, bool first, int t) {
+        if constexpr (DUMP) {  // S^T of tile t as the softmax below reads it (bias removed)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                int32_t* sd = dbg.S + ((size_t)bh * N + (size_t)qg * QMHA_GROUP + 16 * qb + r16) * N + (size_t)t * QMHA_GROUP;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sd[kap16_i8(kb, 4 * grp + i)] = s.v[kb][qb][i] - 0x4B400000;
+            }
+        }
+        v8h vop[DB];  // V^T rows 16 m + r16, slots 8 grp .. +7
+#pragma unroll
+        for (int m = 0; m < DB; ++m) {
+            const int d = 16 * m + r16;
+            vop[m] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 + 16 * swz_pos<64>(d, grp));
+        }
+        if (first) {  // tile 0 sets the base: max(m0 = 0, row max), the exact rule
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) pt_base(qb, fmaxf(m_run[qb], rowmax_xm(s, qb)));
+        }
+        float p[2][8], q[2][8], ts[2];
+        auto softmax_p = [&](int qb) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                p[qb][j] = __builtin_amdgcn_exp2f(fmaf(__int_as_float(s.v[j >> 2][qb][j & 3]), c_pt, -h_k[qb]));
+                q[qb][j] = fmaf(p[qb][j], h_invp[qb], QMHA_MAGIC_RNE);  // Pi = rint(127 p) in the low bits
+            }
+            const float a0 = p[qb][0] + p[qb][1], a1 = p[qb][2] + p[qb][3], a2 = p[qb][4] + p[qb][5], a3 = p[qb][6] + p[qb][7];
+            ts[qb] = (a0 + a1) + (a2 + a3);
+        };
+        softmax_p(0);
+        softmax_p(1);
+        if (!first) {
+            const uint64_t over0 = __builtin_amdgcn_ballot_w64(ts[0] > h_cap[0]);
+            const uint64_t over1 = __builtin_amdgcn_ballot_w64(ts[1] > h_cap[1]);
+            if (over0 | over1) {  // rare (wave-uniform): rebase the queries with a key quarter above the cap
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    const uint64_t over = qb ? over1 : over0;
+                    const float xm = rowmax_xm(s, qb);
+                    const uint32_t q16 = (uint32_t)(over | (over >> 32));
+                    const uint32_t rows = (q16 | (q16 >> 16)) & 0xffffu;
+                    const float mb = ((rows >> r16) & 1u) ? xm : m_run[qb];
+                    const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - mb);
+                    l_run[qb] *= alpha;
+#pragma unroll
+                    for (int m = 0; m < DB; ++m) o[m][qb] *= alpha;
+                    pt_base(qb, mb);
+                    softmax_p(qb);
+                }
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            l_run[qb] = fmaf(ts[qb], h_f[qb], l_run[qb]);  // l = alpha l + sum(p)
+            v4i pw;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                pw[i] = (int)__builtin_amdgcn_perm(__float_as_uint(q[qb][2 * i + 1]), __float_as_uint(q[qb][2 * i]), 0x05040100u);
+            const v8h pop = __builtin_bit_cast(v8h, pw);
+#pragma unroll
+            for (int m = 0; m < DB; ++m) o[m][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vop[m], pop, o[m][qb], 0, 0, 0);
+        }
+    };
+
+    issue(0, 0);
+    qmha_dma_barrier();
+    int t = 0;
+    auto stage = [&](auto BUF, int st) {
+        constexpr int buf = decltype(BUF)::value;
+        if (st + 1 < nst) issue(buf ^ 1, st + 1);
+        if (active) {
+            const char* L = lds[buf];
+            const int ngr = G - st * SG;  // < SG only in a partial last stage (uniform)
+#pragma unroll
+            for (int gi = 0; gi < SG; ++gi) {
+                if (gi == 0 || gi < ngr) tile(L, gi, qk(L, gi), t == 0, st * SG + gi);
+                ++t;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        qmha_dma_barrier();
+    };
+    int st = 0;
+    for (; st + 2 <= nst; st += 2) {
+        stage(std::integral_constant<int, 0>{}, st);
+        stage(std::integral_constant<int, 1>{}, st + 1);
+    }
+    if (st < nst) stage(std::integral_constant<int, 0>{}, st);
+    if (active) {
+        // O is in units of 2^-24 (the f16-subnormal P entries) times sV / 127
+        const float unanchor = 16777216.0f * (sV[bh] / 127.0f);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            float l = l_run[qb];
+            l += __shfl_xor(l, 16);
+            l += __shfl_xor(l, 32);
+            const bool ok = l > 1e-20f;
+            float* orow = O + ((size_t)b * N + (size_t)qg * QMHA_GROUP + 16 * qb + r16) * d_model + (size_t)k * D + 4 * grp;
+#pragma unroll
+            for (int m = 0; m < DB; ++m) {
+                v4f w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = ok ? (o[m][qb][j] * unanchor) / l : 0.0f;
+                *reinterpret_cast<v4f*>(orow + 16 * m) = w;
+            }
+        }
+    }
+}
+
 // ---- per-tensor mode (fa_tc_int8_pt) -----------------------------------------------------
 size_t int8_pt_workspace_bytes(int B, int N, int H, int D) {
     const size_t e = align_up((size_t)B * H * N * D, 256);
@@ -1139,11 +1397,26 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
+template <int D, int WAVES, bool DUMP = false>
+static hipError_t fa_int8_pt_v3_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
+                                       hipStream_t stream, QkDump dbg = QkDump{}) {
+    const int G = N / QMHA_GROUP;
+    const int nqb = (G + WAVES - 1) / WAVES;
+    const float c_log2 = (1.0f / sqrtf((float)D)) * kLog2e;
+    hipLaunchKernelGGL((qmha_fa_int8_pt_v3_kernel<D, WAVES, 2, DUMP>), dim3(B * H * nqb), dim3(WAVES * 64), 0, stream, Qf,
+                       w.Ki, w.Vh, w.sQ, w.sK, w.sV, O, N, H, d_model, nqb, c_log2, dbg);
+    return hipGetLastError();
+}
+
 hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int D,
                                   int d_model, hipStream_t stream) {
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra>(w, Qf, O, B, N, H, d_model, stream);
-        case 64: return fa_int8_pt_launch<64, kD64Flags>(w, Qf, O, B, N, H, d_model, stream);
+        // d = 64: the 16x16 kernel (v3), same box, alternating: C4 -4.4 %, B = 2 -6.7 %, but B = 1 +7.2 %
+        // (256 workgroups = 2 waves per SIMD, which the unpipelined tile cannot hide latency with).  At
+        // d = 128 it measured +1.6 % (193 VGPRs, 2 waves per SIMD), so the scheduled pipe kernel keeps
+        // d = 32 / 128 (profiles/r06/ab_pt_mma16/)
+        case 64: return fa_int8_pt_v3_launch<64, 8>(w, Qf, O, B, N, H, d_model, stream);
         case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
@@ -1182,7 +1455,7 @@ hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float
                                   int d_model, QkDump dbg, hipStream_t stream) {
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
-        case 64: return fa_int8_pt_launch<64, kD64Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 64: return fa_int8_pt_v3_launch<64, 8, true>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 128: return fa_int8_pt_launch<128, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         default: return hipErrorInvalidValue;
     }

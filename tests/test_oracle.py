@@ -218,6 +218,11 @@ def _tree_sum16_rows(p):
     return (a + b) + (c + d)
 
 
+def _tree_sum8_rows(p):
+    """The 16x16 kernels' eight-key tree: ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7))."""
+    return ((p[:, 0] + p[:, 1]) + (p[:, 2] + p[:, 3])) + ((p[:, 4] + p[:, 5]) + (p[:, 6] + p[:, 7]))
+
+
 def _np_fa_int8_pt(Q, K, V, h):
     """numpy restatement of oracle_fa_int8_pt for one sequence (base 2, the kernel's score constant;
     float32 arithmetic except x = S * c - m, rounded once from float64 like the kernel's fma)."""
@@ -233,12 +238,16 @@ def _np_fa_int8_pt(Q, K, V, h):
             qs.append((np.clip(np.rint(X[:, sl] * (f(1.0) / s)), -128, 127).astype(np.int64), s))
         (Qi, sQ), (Ki, sK), (Vi, sV) = qs
         c = _pt_score_constant(sQ, sK, d)
-        halves = [np.array([(i & 3) + 8 * (i >> 2) + 4 * hh for i in range(16)]) for hh in range(2)]
+        if d == 64:  # the 16x16 kernel's lane quarters (keys kap16(j >> 2, 4 g + (j & 3)), pairwise tree)
+            halves = [np.array([16 * ((4 * g + (j & 3)) >> 3) + 4 * (((4 * g + (j & 3)) >> 2) & 1) + (j & 3) + 8 * (j >> 2)
+                                for j in range(8)]) for g in range(4)]
+        else:  # the 32x32 kernel's lane halves
+            halves = [np.array([(i & 3) + 8 * (i >> 2) + 4 * hh for i in range(16)]) for hh in range(2)]
         cap = f(2047.0) / f(127.0)
         for g in range(N // 32):
             rows = slice(32 * g, 32 * g + 32)
             O = np.zeros((32, d), f)
-            l = np.zeros((32, 2), f)
+            l = np.zeros((32, len(halves)), f)
             m = np.zeros(32, f)
             for t in range(N // 32):
                 cols = slice(32 * t, 32 * t + 32)
@@ -250,7 +259,8 @@ def _np_fa_int8_pt(Q, K, V, h):
                 def tile_p(base):
                     x = (S.astype(np.float64) * np.float64(c) - base[:, None].astype(np.float64)).astype(f)
                     p = np.exp2(x).astype(f)
-                    return p, np.stack([_tree_sum16_rows(p[:, hv]) for hv in halves], axis=1)
+                    return p, np.stack([_tree_sum16_rows(p[:, hv]) if len(hv) == 16 else _tree_sum8_rows(p[:, hv])
+                                        for hv in halves], axis=1)
                 p, ts = tile_p(m)
                 alpha = np.ones(32, f)
                 if t > 0:  # ... later tiles move it to the row max when a key half sums above the cap
@@ -262,14 +272,15 @@ def _np_fa_int8_pt(Q, K, V, h):
                 l = (alpha[:, None] * l + ts).astype(f)
                 Pi = np.minimum(np.rint(p * f(127.0)), 2047).astype(np.int64)
                 O = O * alpha[:, None] + (Pi @ Vi[cols]).astype(f)
-            l = l[:, 0] + l[:, 1]
+            l = (l[:, 0] + l[:, 1]) + (l[:, 2] + l[:, 3]) if len(halves) == 4 else l[:, 0] + l[:, 1]
             out[rows, sl] = np.where(l[:, None] > 1e-20, O * (sV / f(127.0)) / l[:, None], 0)
     return out
 
 
-def test_fa_int8_pt_matches_numpy_restatement(oracle_mod):
+@pytest.mark.parametrize("dm", [64, 128])  # d = 32 (lane halves) and d = 64 (the 16x16 kernel's quarters)
+def test_fa_int8_pt_matches_numpy_restatement(oracle_mod, dm):
     rng = np.random.default_rng(13)
-    N, dm, h = 128, 64, 2
+    N, h = 128, 2
     Q, K, V = (rng.standard_normal((N, dm)).astype(np.float32) for _ in range(3))
     got = oracle_mod.fa_int8_pt(Q, K, V, dm, h)
     ref = _np_fa_int8_pt(Q, K, V, h)
