@@ -356,7 +356,8 @@ def isa_ids(variant, d):
     digits of the SHA-256 of their gfx950 instruction bytes in the loaded libqmha.so (quantizedmha_amd/isa_id.py)."""
     from quantizedmha_amd import isa_id
     pats = {"fa_tc_int8_b": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_quant_int8_kernelILi{d}ELi1E"),
-            "fa_tc_int8_pt": (f"qmha_fa_int8_pipe_kernelILi{d}E", f"qmha_pt_quant_kernelILi{d}E"),
+            "fa_tc_int8_pt": (f"qmha_fa_int8_pt_v3_kernelILi{d}ELi8ELi2ELb0E" if d == 64 else f"qmha_fa_int8_pipe_kernelILi{d}E",
+                              f"qmha_pt_quant_kernelILi{d}E"),
             "fa_tc_v1a": (f"qmha_fa_f16_{'v3' if d in (64, 128) else 'v2'}_kernelILi{d}E", f"qmha_convert_f16_kernelILi{d}E"),
             "fa": (f"qmha_fa_f32_v3_kernelILi{d}E", None), "fa_mfma": (f"qmha_fa_f32_mfma_kernelILi{d}E", None),
             "unfused": ("qmha_gemm_f32_mfma_kernel", "qmha_softmax_rows")}.get(variant, (None, None))
@@ -370,7 +371,7 @@ def isa_ids(variant, d):
             keep = {}
             for name, b in ks.items():
                 fl = re.search(r"ILi\d+ELi\d+ELi(\d+)E", name)
-                if role == "main" and fl and (int(fl.group(1)) & 256 or bool(int(fl.group(1)) & (1 << 20)) != want_pt):
+                if role == "main" and "pipe_kernel" in name and fl and (int(fl.group(1)) & 256 or bool(int(fl.group(1)) & (1 << 20)) != want_pt):
                     continue
                 keep[name] = b
             ks = keep

@@ -22,7 +22,7 @@ find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 find $OUT/trace -name "*kernel_trace.csv" -exec cp {} $OUT/kernel_trace.csv \;
 rm -rf $OUT/trace
 python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64ELi4ELi65E" 30 50 > $OUT/trace_window.txt
-python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pipe_kernelILi64ELi4ELi1048641E" 2 25 >> $OUT/trace_window.txt
+python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_int8_pt_v3_kernelILi64ELi8ELi2ELb0E" 2 25 >> $OUT/trace_window.txt
 python3 tools/trace_window.py $OUT/kernel_trace.csv "qmha_fa_f16_v3_kernelILi64" 10 25 >> $OUT/trace_window.txt
 cat $OUT/trace_window.txt
 exit 0
