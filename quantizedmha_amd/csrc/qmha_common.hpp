@@ -110,6 +110,23 @@ __device__ __forceinline__ int swz_src(int row, int j) {
     else return (j + cpr - swz_rot<RB>(row)) % cpr;
 }
 
+// LDS chunk swizzles of the 16x16-MFMA kernels (qmha_fa_f16.hip v3, qmha_fa_int8.hip pt v3): slot =
+// chunk ^ swz(row).  A ds_read_b128 lane group (16 lanes: one 256-byte bank row) reads, in the kap16 key
+// order, K rows {0-3, 20-23} at chunk c and {4-7, 16-19} at chunk c ^ 1 (+8 kb), and V^T rows (d)
+// r16 = {0-3, 12-15} at chunk g and {4-11} at chunk g ^ 1.  swz_rot's (row / rows-per-bank-row) puts two
+// of those four row quads on the same slots (2-way: SQ_LDS_BANK_CONFLICT was half of all LDS cycles);
+// these XOR masks give every lane of a group its own 16-byte slot (checked exhaustively in
+// tests/test_abi.py::test_lds_swizzle16_conflict_free).
+template <int RB>
+__host__ __device__ constexpr int kswz16(int row) {
+    static_assert(RB == 64 || RB == 128 || RB == 256, "64 / 128 / 256-byte K rows");
+    if constexpr (RB == 64) return 2 * ((row >> 4) & 1);
+    else if constexpr (RB == 128) return ((row >> 1) & 1) ^ (2 * ((row >> 2) & 1)) ^ (4 * ((row >> 4) & 1));
+    else return (row & 1) ^ (2 * ((row >> 1) & 1)) ^ (4 * ((row >> 2) & 1)) ^ (8 * ((row >> 4) & 1));
+}
+// V^T operand rows: 64 bytes (32 keys of f16) per d row
+__host__ __device__ constexpr int vswz16(int d) { return (2 * ((d >> 2) & 1)) ^ (3 * ((d >> 3) & 1)); }
+
 // --------------------------------------------------------------------------
 // cross-lane helpers (wave64)
 // --------------------------------------------------------------------------

@@ -335,14 +335,14 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_f16_v3_ker
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
-        const int row = idx / (RB / 16), cc = swz_src<RB>(row, idx % (RB / 16));
+        const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ kswz16<RB>(row);
         koff[jj] = row * RB + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
         const int gq = idx / (4 * D), w = idx % (4 * D);
-        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
+        const int d = w >> 2, cv = (w & 3) ^ vswz16(d);
         voff[jj] = gq * 64 * D + d * 64 + 16 * cv;
     }
     auto issue = [&](int buf, int st) {
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_f16_v3_ker
             s.v[kb][0] = s.v[kb][1] = v4f{};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * swz_pos<RB>(krow, 4 * ks + grp));
+                const v8h kop = *reinterpret_cast<const v8h*>(L + krow * RB + 16 * ((4 * ks + grp) ^ kswz16<RB>(krow)));
 #pragma unroll
                 for (int qb = 0; qb < 2; ++qb) s.v[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kop, qop[qb][ks], s.v[kb][qb], 0, 0, 0);
             }
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_f16_v3_ker
 #pragma unroll
         for (int m = 0; m < DB; ++m) {
             const int d = 16 * m + r16;
-            vop[m] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 + 16 * swz_pos<64>(d, grp));
+            vop[m] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 + 16 * (grp ^ vswz16(d)));
         }
         float p[2][8];
         float ts[2];

@@ -1180,14 +1180,14 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_int8_pt_v3
 #pragma unroll
     for (int jj = 0; jj < KJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
-        const int row = idx / (RB / 16), cc = swz_src<RB>(row, idx % (RB / 16));
+        const int row = idx / (RB / 16), cc = (idx % (RB / 16)) ^ kswz16<RB>(row);
         koff[jj] = row * RB + 16 * cc;
     }
 #pragma unroll
     for (int jj = 0; jj < VJ; ++jj) {
         const int idx = (wave + jj * WAVES) * 64 + lane;
         const int gq = idx / (4 * D), w = idx % (4 * D);
-        const int d = w >> 2, cv = swz_src<64>(d, w & 3);
+        const int d = w >> 2, cv = (w & 3) ^ vswz16(d);
         voff[jj] = gq * 64 * D + d * 64 + 16 * cv;
     }
     auto issue = [&](int buf, int st) {
@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_int8_pt_v3
             const int krow = gi * 32 + kap16_i8(kb, r16);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const v4i kop = *reinterpret_cast<const v4i*>(L + krow * RB + 16 * swz_pos<RB>(krow, 4 * ks + grp));
+                const v4i kop = *reinterpret_cast<const v4i*>(L + krow * RB + 16 * ((4 * ks + grp) ^ kswz16<RB>(krow)));
 #pragma unroll
                 for (int qb = 0; qb < 2; ++qb)
                     s.v[kb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(kop, qop[qb][ks], ks == 0 ? magic4 : s.v[kb][qb], 0, 0, 0);
@@ -1246,7 +1246,7 @@ __global__ __launch_bounds__(WAVES * 64, D > 64 ? 2 : 4) void qmha_fa_int8_pt_v3
 #pragma unroll
         for (int m = 0; m < DB; ++m) {
             const int d = 16 * m + r16;
-            vop[m] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 + 16 * swz_pos<64>(d, grp));
+            vop[m] = *reinterpret_cast<const v8h*>(L + KBYTES + gi * 64 * D + d * 64 + 16 * (grp ^ vswz16(d)));
         }
         if (first) {  // tile 0 sets the base: max(m0 = 0, row max), the exact rule
 #pragma unroll
@@ -1397,6 +1397,10 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
+#ifndef QMHA_PT_V3_WAVES
+#define QMHA_PT_V3_WAVES 8  // A/B builds: -DQMHA_PT_V3_WAVES=4
+#endif
+
 template <int D, int WAVES, bool DUMP = false>
 static hipError_t fa_int8_pt_v3_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
                                        hipStream_t stream, QkDump dbg = QkDump{}) {
@@ -1416,7 +1420,7 @@ hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float
         // (256 workgroups = 2 waves per SIMD, which the unpipelined tile cannot hide latency with).  At
         // d = 128 it measured +1.6 % (193 VGPRs, 2 waves per SIMD), so the scheduled pipe kernel keeps
         // d = 32 / 128 (profiles/r06/ab_pt_mma16/)
-        case 64: return fa_int8_pt_v3_launch<64, 8>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: return fa_int8_pt_v3_launch<64, QMHA_PT_V3_WAVES>(w, Qf, O, B, N, H, d_model, stream);
         case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
@@ -1455,7 +1459,7 @@ hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float
                                   int d_model, QkDump dbg, hipStream_t stream) {
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
-        case 64: return fa_int8_pt_v3_launch<64, 8, true>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 64: return fa_int8_pt_v3_launch<64, QMHA_PT_V3_WAVES, true>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 128: return fa_int8_pt_launch<128, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         default: return hipErrorInvalidValue;
     }
