@@ -1397,9 +1397,18 @@ static hipError_t fa_int8_d(const Int8Workspace& w, const float* Qf, float* O, i
     else return fa_int8_launch<D, kAnyFlags<D> | XFL>(w, Qf, O, B, N, H, d_model, stream, dbg);
 }
 
-#ifndef QMHA_PT_V3_WAVES
-#define QMHA_PT_V3_WAVES 8  // A/B builds: -DQMHA_PT_V3_WAVES=4
-#endif
+// compute units of the current device (cached per device); 0 if unknown
+static long long device_cus() {
+    static std::atomic<int> cus_of[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int c = cus_of[dev].load(std::memory_order_relaxed);
+    if (c <= 0) {
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return 0;
+        cus_of[dev].store(c, std::memory_order_relaxed);
+    }
+    return c;
+}
 
 template <int D, int WAVES, bool DUMP = false>
 static hipError_t fa_int8_pt_v3_launch(const Int8Workspace& w, const float* Qf, float* O, int B, int N, int H, int d_model,
@@ -1420,7 +1429,15 @@ hipError_t launch_fa_int8_pt_main(const Int8Workspace& w, const float* Qf, float
         // (256 workgroups = 2 waves per SIMD, which the unpipelined tile cannot hide latency with).  At
         // d = 128 it measured +1.6 % (193 VGPRs, 2 waves per SIMD), so the scheduled pipe kernel keeps
         // d = 32 / 128 (profiles/r06/ab_pt_mma16/)
-        case 64: return fa_int8_pt_v3_launch<64, QMHA_PT_V3_WAVES>(w, Qf, O, B, N, H, d_model, stream);
+        case 64: {
+            // 8-wave workgroups; grids of at most one such workgroup per CU (2 waves per SIMD, e.g. one
+            // sequence of H16 N4096) run 4-wave ones instead, whose two workgroups per CU do not share a
+            // barrier phase: same box, alternating, B1 N4096 H16 -2.0 %, B1 N8192 H8 -2.6 %, but B2 +6 %
+            // and C4 +2.6 % (profiles/r06/ab_pt_mma16/w4/).  WAVES changes no value: bit-identical.
+            const long long wgs8 = (long long)B * H * ((N / QMHA_GROUP + 7) / 8), cus = device_cus();
+            if (cus > 0 && wgs8 <= cus) return fa_int8_pt_v3_launch<64, 4>(w, Qf, O, B, N, H, d_model, stream);
+            return fa_int8_pt_v3_launch<64, 8>(w, Qf, O, B, N, H, d_model, stream);
+        }
         case 128: return fa_int8_pt_launch<128, kD128Flags>(w, Qf, O, B, N, H, d_model, stream);
         default: return hipErrorInvalidValue;
     }
@@ -1459,7 +1476,7 @@ hipError_t launch_fa_int8_pt_dump(const Int8Workspace& w, const float* Qf, float
                                   int d_model, QkDump dbg, hipStream_t stream) {
     switch (D) {
         case 32: return fa_int8_pt_launch<32, kD32Flags | kPtD32Extra | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
-        case 64: return fa_int8_pt_v3_launch<64, QMHA_PT_V3_WAVES, true>(w, Qf, O, B, N, H, d_model, stream, dbg);
+        case 64: return fa_int8_pt_v3_launch<64, 8, true>(w, Qf, O, B, N, H, d_model, stream, dbg);
         case 128: return fa_int8_pt_launch<128, kD128Flags | FL_DUMP>(w, Qf, O, B, N, H, d_model, stream, dbg);
         default: return hipErrorInvalidValue;
     }

@@ -192,12 +192,17 @@ def test_production_library_has_one_kernel_per_variant_and_d(built):
     # per-tensor d = 32 / 64 / 128
     assert len(dumps) == 11, dumps
     for name, d, twin in dumps:  # exactly the production schedule (same WAVES, flags, PAD) plus the stores
-        assert per[(name, d)] == {twin}, (name, d, twin)
+        if name == "qmha_fa_int8_pt_v3_kernel":  # the 8-wave production instance (the 4-wave one has no twin)
+            assert twin in per[(name, d)], (name, d, twin)
+        else:
+            assert per[(name, d)] == {twin}, (name, d, twin)
     assert per, syms[:2000]
     for (name, d), inst in per.items():
         # the V layout and the per-tensor mode are template arguments of the quantiser; the any-d
         # pre-pass is instantiated for the int8 V layouts and the fp16 conversion
         limit = 3 if name in ("qmha_quant_int8_kernel", "qmha_prepass_any_kernel") else 1
+        if name == "qmha_fa_int8_pt_v3_kernel":  # 8-wave workgroups, 4-wave ones for one-CU-each grids
+            limit = 2
         assert len(inst) <= limit, (name, d, sorted(inst))
     blob = open(path, "rb").read()
     for env in (b"QMHA_INT8_CFG", b"QMHA_F16_CFG", b"QMHA_F32_CFG", b"QMHA_OVERLAP_CHUNKS", b"QMHA_INT8_ABL"):
